@@ -1,0 +1,790 @@
+/* ORACLE — test infrastructure only.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library; the product path
+ * (mh-ppo_amd/) never links or calls it.
+ *
+ * Literal CPU restatement of the reference crosswalk environments, one env
+ * per handle, each with its own CPython-`random` stream (the reference runs
+ * one env on the module-global stream; swapping that stream per env is how
+ * the golden fixtures were captured, tests/golden/gen/make_env_golden.py).
+ *
+ * Follows, statement by statement (file:line, reference under
+ * /root/reference/Environments):
+ *   pedestrian.__init__   Env_hybrid_multi_coop.py:15-103   (variants noted)
+ *   choix_pedestrian      Env_hybrid_multi_coop.py:138-173  (naif :129-174, 4cars :255-289)
+ *   detection             Env_hybrid_multi_coop.py:175-259  (scalable :176-264, naif :176-215)
+ *   boolean_ped_position  Env_hybrid_multi_coop.py:261-274
+ *   will/apply_change_line Env_hybrid_multi_coop.py:276-289
+ *   pedestrian.step       Env_hybrid_multi_coop.py:292-401  (scalable mid-cross stop :371-380)
+ *   CG_score              Env_hybrid_multi_coop.py:403-412
+ *   new_pedestrian_*      Env_hybrid_multi_coop.py:414-427
+ *   get_data / is_in_front / is_crossing_in_front / new_reward_wait_safety /
+ *   delta_l_all / delta_l / worst_delta_l    Env_hybrid_multi_coop.py:433-511
+ *   car.__init__/step/sigma/get_data/rewards Env_hybrid_multi_coop.py:515-622
+ *   car.follow_action (IDM)  Env_hybrid_multi_coop_scalable.py:604-624
+ *   car_follower             Env_hybrid_multi_coop_4cars.py:13-129
+ *   env.step               Env_hybrid_multi_coop.py:745-832 (4cars :783-844, scalable :789-878)
+ *   env.reset              Env_hybrid_multi_coop.py:838-893 (4cars :850-911, scalable :884-946)
+ * libm calls are glibc's, exactly what CPython's `math` module calls.
+ * Compile with -ffp-contract=off (no FMA contraction): every expression keeps
+ * Python's left-to-right evaluation and rounding.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pyrandom.h"
+
+enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3 };
+#define MAXC 16
+#define MAXP 8
+
+static const double PI = 0x1.921fb54442d18p+1; /* math.pi */
+
+/* Python's two-argument min/max: the first argument wins unless the second
+ * compares strictly smaller/greater (NaN semantics included). */
+static double pymin(double a, double b) { return (b < a) ? b : a; }
+static double pymax(double a, double b) { return (b > a) ? b : a; }
+
+/* CPython float floor division (Objects/floatobject.c _float_div_mod) */
+static double py_floordiv(double vx, double wx) {
+    double mod = fmod(vx, wx);
+    double div = (vx - mod) / wx;
+    double floordiv;
+    if (mod) {
+        if ((wx < 0) != (mod < 0)) { mod += wx; div -= 1.0; }
+    }
+    if (div) {
+        floordiv = floor(div);
+        if (div - floordiv > 0.5) floordiv += 1.0;
+    } else {
+        floordiv = copysign(0.0, vx / wx);
+    }
+    return floordiv;
+}
+
+typedef struct {
+    double worst_dl, cross, cross_lines;
+    int max_lines;
+    double dt;
+    int decision, at_crossing, ped_left, ped_in_cross, accident, is_crossing;
+    int time_to_remove;
+    double time_before_crossing, waiting_time, crossing_time;
+    int worst_scenario_accident, follow_rule, exist;
+    double Vm, tau;
+    int direction;
+    double line_pos;
+    double init_speed[2], init_pos[2], ratio;
+    double Vp_x, Vp_y, Sp_x, Sp_y;
+    int time_stop, stop;
+    double t0;
+    int gender, age;
+    double CG;
+    int change_line;
+    double delta;
+    int need_to_stop;
+    double cross_stop;
+    int sin_model;
+    double t_init, T, A, B, w;
+    int choose;
+} Ped;
+
+typedef struct {
+    double dt, cross, cross_lines, line, light;
+    double Ac, Vc, Sc;
+    double initial_speed;
+    double acc_hist[2]; /* previous_acc deque [-2], [-3] (discount 0) */
+    double possible_accident, error_scenario, Ts, time_braking;
+    int exist;
+} Car;
+
+typedef struct {
+    int variant, nb_car, nb_ped, nb_lines, max_episode, sin_model;
+    double dt, car_b[2][2], ped_b[2][4], cross_b[2];
+    PyRandom rng;
+    double cross;
+    int speed_limit;
+    int nS;       /* car slots on the AV list (coop/naif nb_car, 4cars nb_car, scalable 2L) */
+    Car cars[MAXC];
+    Car follow[MAXC]; /* 4cars only */
+    Ped peds[MAXP];
+    int ped_traffic, car_traffic;
+    double time, episode_length;
+    double reward_light[MAXC];
+} OEnv;
+
+/* ---------------------------------------------------------------- ped -- */
+
+static double ped_CG_score(OEnv *e, Ped *p, double crossing_size) {
+    if (!p->is_crossing) return 0.;
+    const double fem = 0.0369, child = -0.0355, midage = -0.0221, old = -0.1810;
+    const double alpha = 0.09, sigma = 0.09;
+    double gamma = log10(crossing_size / fabs(p->init_speed[1] + 10e-3));
+    double log_val = alpha + gamma + fem * (double)(p->gender == 1) + child * (double)(p->age == 0) +
+                     midage * (double)(p->age == 1) + old * (double)(p->age == 2);
+    log_val = log_val + pyr_normalvariate(&e->rng, 0.0, sigma);
+    return pow(10.0, log_val);
+}
+
+static void ped_init(OEnv *e, Ped *p, int is_crossing, int exist) {
+    PyRandom *r = &e->rng;
+    const int v = e->variant;
+    memset(p, 0, sizeof(*p));
+    p->worst_dl = 0.0;
+    p->cross = e->cross;
+    p->cross_lines = (double)e->nb_lines * e->cross;
+    p->max_lines = e->nb_lines;
+    p->dt = e->dt;
+    p->is_crossing = is_crossing;
+    p->time_to_remove = (int)pyr_randint(r, 0, 20);
+    p->follow_rule = pyr_randint(r, 0, 9) < (v == V_NAIF ? 10 : 3);
+    p->exist = exist;
+    p->Vm = 2.5;
+    p->tau = 1.0;
+    p->direction = 2 * (int)pyr_randint(r, 0, 1) - 1;
+    p->line_pos = (double)(p->max_lines * (p->direction < 0) - 1 * (p->direction > 0));
+    p->init_speed[0] = pyr_uniform(r, e->ped_b[0][0], e->ped_b[1][0]);
+    p->init_speed[1] = pyr_uniform(r, e->ped_b[0][1], e->ped_b[1][1]) * (double)p->direction;
+    p->init_pos[0] = pyr_uniform(r, e->ped_b[0][2], e->ped_b[1][2]);
+    p->init_pos[1] = (pyr_uniform(r, e->ped_b[0][3], e->ped_b[1][3]) - p->cross_lines / 2.) * (double)p->direction;
+    p->ratio = 0.0;
+    if (!p->exist) {
+        p->init_speed[0] = 0.; p->init_speed[1] = 0.;
+        if (v == V_4CARS || v == V_NAIF) {
+            p->init_pos[0] = e->ped_b[0][2];
+            p->init_pos[1] = e->ped_b[0][3] * (double)p->direction;
+        } else {
+            p->init_pos[1] = e->ped_b[0][3] * (double)p->direction;
+        }
+    } else if (!p->is_crossing) {
+        p->init_speed[0] = 0.; p->init_speed[1] = 0.;
+        p->direction = 0;
+    } else {
+        p->ratio = p->init_speed[0] / p->init_speed[1];
+    }
+    p->Vp_x = p->init_speed[0]; p->Vp_y = p->init_speed[1];
+    p->Sp_x = p->init_pos[0]; p->Sp_y = p->init_pos[1];
+    p->time_stop = 0; p->stop = 0; p->t0 = 0.0;
+    p->gender = (int)pyr_randint(r, 0, 1);
+    p->age = (int)pyr_randint(r, 0, 2);
+    p->CG = ped_CG_score(e, p, p->cross);
+    p->change_line = 0;
+    p->delta = 0.0;
+    if (v == V_COOP) {
+        p->need_to_stop = 1;
+        p->cross_stop = pyr_uniform(r, -p->cross_lines / 2 + 0.2, p->cross_lines / 2 - 0.2);
+    } else if (v == V_SCALABLE) {
+        p->need_to_stop = pyr_uniform(r, 0, 1) < 0.5;
+        p->cross_stop = pyr_uniform(r, -p->cross_lines / 2 + 0.2, p->cross_lines / 2 - 0.2);
+    }
+    p->sin_model = e->sin_model && p->is_crossing;
+    if (p->sin_model) {
+        p->t_init = 0.0;
+        double abs_speed = fabs(p->init_speed[1]);
+        p->T = p->cross_lines / (abs_speed + 10e-3);
+        int check = ((abs_speed * PI) / 2.0 <= p->Vm);
+        p->A = (double)check * PI * abs_speed / 2.0 + (double)(!check) * (p->Vm - abs_speed) / (1.0 - (2.0 / PI));
+        p->B = (double)(!check) * (p->Vm - p->A);
+        p->w = PI / p->T;
+    }
+}
+
+static int is_in_front(const Ped *p, double car_line, double next_line) {
+    double line_1 = (-p->cross_lines / 2) + p->cross * (car_line - 0.5 * next_line + 1);
+    double line_2 = (p->cross_lines / 2) - p->cross * ((double)p->max_lines - 0.5 * next_line - car_line);
+    if (p->direction == -1) return p->Sp_y >= line_2 - 0.001;
+    return p->Sp_y <= line_1 + 0.001;
+}
+
+static int is_crossing_in_front(const Ped *p, double car_line, double prev_line) {
+    double line_1 = (-p->cross_lines / 2) + p->cross * (car_line - prev_line);
+    double line_2 = (p->cross_lines / 2) - p->cross * ((double)p->max_lines - car_line - 1 - prev_line);
+    if (p->direction == -1) return p->Sp_y < line_2;
+    return p->Sp_y > line_1;
+}
+
+static void unif_y(const Ped *p, double *pos, double *spd) {
+    *pos = p->Sp_y + p->init_speed[1] * p->dt;
+    *spd = p->init_speed[1];
+}
+
+static void sin_y(const Ped *p, double time, double *pos, double *spd) {
+    double t = time + p->dt;
+    double speed_p = (p->A * sin(p->w * (t - p->t0)) + p->B);
+    double pos_p = ((-p->cross_lines / 2.) + (p->A * (-cos(p->w * (t - p->t0)) + cos(p->w * p->t_init)) / p->w));
+    if (pos_p >= 0.0 && speed_p < fabs(p->init_speed[1])) {
+        unif_y(p, pos, spd);
+        return;
+    }
+    *pos = (double)p->direction * pos_p;
+    *spd = (double)p->direction * speed_p;
+}
+
+static void function_step(const Ped *p, double time, double *pos, double *spd) {
+    if (p->sin_model) sin_y(p, time, pos, spd);
+    else unif_y(p, pos, spd);
+}
+
+/* cars_* lists as seen by the pedestrian (env-specific filtering done by caller) */
+typedef struct {
+    int n;
+    double speed[2 * MAXC], pos[2 * MAXC], line[2 * MAXC], light[2 * MAXC];
+} CarView;
+
+static int choix_pedestrian(OEnv *e, Ped *p, const CarView *cv) {
+    const int v = e->variant;
+    const double car_size = 4;
+    int n = cv->n;
+    if (p->follow_rule) {
+        int cars[2 * MAXC];
+        for (int i = 0; i < n; i++) cars[i] = i;
+        if (v == V_NAIF) {
+            if (n > 1) pyr_shuffle(&e->rng, cars, n);
+            for (int k = 0; k < n; k++) {
+                int i = cars[k];
+                if (is_crossing_in_front(p, cv->line[i], 0.5) * is_in_front(p, cv->line[i], 1.0) *
+                    (cv->pos[i] < car_size + p->Sp_x) * (cv->pos[i] > p->Sp_x))
+                    return 0;
+            }
+            for (int k = 0; k < n; k++) {
+                int i = cars[k];
+                if (cv->pos[i] < p->Sp_x && cv->light[i] < 0) return 0;
+            }
+        } else {
+            if (v != V_4CARS && n > 1) {
+                int tmp[2 * MAXC];
+                for (int i = 0; i < n; i++) tmp[i] = i;
+                pyr_shuffle(&e->rng, tmp, n); /* throw-away list: RNG consumption only */
+            }
+            for (int i = 0; i < n; i++) {
+                if (is_crossing_in_front(p, cv->line[i], 0.5) * is_in_front(p, cv->line[i], 1.0)) {
+                    if ((cv->pos[i] < car_size + p->Sp_x) * (cv->pos[i] > p->Sp_x)) return 0;
+                }
+            }
+            for (int i = 0; i < n; i++) {
+                if (cv->pos[i] < p->Sp_x && cv->light[i] != 0) return cv->light[i] > 0.;
+            }
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        if (is_in_front(p, cv->line[i], 1.0)) {
+            if ((cv->pos[i] < car_size + p->Sp_x) * (cv->pos[i] > p->Sp_x)) return 0;
+            if (cv->pos[i] < p->Sp_x) {
+                double car_time = fabs((cv->pos[i] - p->Sp_x) / (cv->speed[i] + 10e-3));
+                double CG = ped_CG_score(e, p, fabs(p->line_pos - cv->line[i]) * p->cross);
+                if (car_time + cv->light[i] < CG) return 0;
+            }
+        }
+    }
+    return 1;
+}
+
+static double worst_delta_l(const OEnv *e, const Ped *p, double car_pos, double car_speed, double car_line) {
+    if (car_pos > p->Sp_x || p->ped_left || !is_in_front(p, car_line, 0))
+        return e->variant == V_SCALABLE ? 100.0 : 0.0;
+    return fabs(car_pos - p->Sp_x) - (car_speed * car_speed / (-2.0 * e->car_b[0][0]));
+}
+
+static double delta_l(const OEnv *e, const Ped *p, double car_pos, double car_speed, double car_line) {
+    if (car_pos > p->Sp_x || p->ped_left || !is_in_front(p, car_line, 0)) return 0.0;
+    return fabs(car_pos - p->Sp_x) - (car_speed * car_speed / (-2.0 * e->car_b[0][0])) - p->tau * (car_speed);
+}
+
+static double delta_l_all(const OEnv *e, const Ped *p, const CarView *cv) {
+    double dl = e->variant == V_SCALABLE ? 100.0 : 0.0;
+    for (int i = 0; i < cv->n; i++) {
+        if ((cv->pos[i] <= p->Sp_x) && is_in_front(p, cv->line[i], 0) && (!p->ped_left) && (cv->light[i] >= 0)) {
+            double nd = fabs(cv->pos[i] - p->Sp_x) - (cv->speed[i] * cv->speed[i] / (-2.0 * e->car_b[0][0])) -
+                        p->tau * (cv->speed[i]);
+            dl = pymin(dl, nd);
+        }
+    }
+    return dl;
+}
+
+static void ped_get_data(const OEnv *e, Ped *p, const CarView *cv, double out[9]) {
+    if (!p->exist) {
+        for (int k = 0; k < 9; k++) out[k] = 0.;
+        return;
+    }
+    p->delta = pymin(delta_l_all(e, p, cv) * (double)p->is_crossing * (double)(!p->ped_left), p->delta);
+    out[0] = p->Vp_x; out[1] = p->Vp_y; out[2] = p->Sp_x; out[3] = p->Sp_y; out[4] = p->delta;
+    out[5] = p->ped_left; out[6] = p->ped_in_cross; out[7] = p->exist; out[8] = p->direction;
+}
+
+static double new_reward_wait_safety(const OEnv *e, Ped *p, double car_speed, double car_pos, double car_line) {
+    if ((!p->ped_left) * (p->is_crossing) * (car_pos < p->Sp_x) * is_in_front(p, car_line, 0)) {
+        double exp_dl;
+        if (car_speed < 0.05) {
+            exp_dl = 0.;
+        } else {
+            double dl = delta_l(e, p, car_pos, car_speed, car_line) / (car_speed);
+            if (dl >= -1.) exp_dl = pymax(-20. * exp(-4. * (dl)-4.), -20.0);
+            else exp_dl = 20. * dl;
+        }
+        exp_dl = exp_dl - (double)(p->accident * 20);
+        if (exp_dl < p->worst_dl) p->worst_dl = exp_dl;
+    }
+    return p->worst_dl + 0.0;
+}
+
+static void boolean_ped_position(Ped *p) {
+    double ds = (double)p->direction * p->Sp_y;
+    if (ds >= p->cross_lines / 2) { p->ped_in_cross = 0; p->ped_left = 1; }
+    else if (ds > -p->cross_lines / 2) { p->ped_in_cross = 1; p->ped_left = 0; }
+    else { p->ped_in_cross = 0; p->ped_left = 0; }
+    if (p->ped_left) p->time_to_remove = p->time_to_remove - 1;
+}
+
+static void will_change_line(Ped *p, double pos, double new_pos) {
+    if (fabs(new_pos) < p->cross_lines / 2) {
+        double new_line = py_floordiv(new_pos + p->cross_lines / 2, p->cross);
+        if (new_line != p->line_pos)
+            if (fabs(pos) < p->cross_lines / 2) p->change_line = 1;
+    }
+}
+
+static void apply_change_line(Ped *p, double pos, double new_pos) {
+    (void)pos;
+    if (fabs(new_pos) >= p->cross_lines / 2) {
+        p->line_pos = (double)(p->max_lines * (p->direction < 0) - 1 * (p->direction > 0));
+    } else {
+        double new_line = py_floordiv(new_pos + p->cross_lines / 2, p->cross);
+        if (new_line != p->line_pos) p->line_pos = new_line;
+    }
+}
+
+static void ped_step(OEnv *e, Ped *p, double time, const CarView *cv) {
+    PyRandom *r = &e->rng;
+    double pp_y, pp_vy;
+    unif_y(p, &pp_y, &pp_vy);
+    boolean_ped_position(p);
+    if (p->Sp_y * (double)p->direction <= (-p->cross_lines / 2)) {
+        p->time_before_crossing = p->time_before_crossing + p->dt;
+    }
+    if (!p->is_crossing) return;
+    p->choose = 1;
+    if ((!p->decision) * (p->at_crossing)) {
+        p->choose = choix_pedestrian(e, p, cv);
+        if (p->choose) {
+            p->line_pos = (double)((p->max_lines - 1) * (p->direction < 0));
+            p->at_crossing = 0;
+        }
+        p->decision = 1;
+        p->t0 = time;
+    }
+    const double dir = (double)p->direction;
+    if ((p->Sp_y * dir < -p->cross_lines / 2.) * (pp_y * dir > -p->cross_lines / 2.) * (!p->decision)) {
+        double pos_p_x = (p->Vp_x * p->dt) * (fabs(-p->cross_lines / 2. - p->Sp_y * dir) / fabs(p->Vp_y * p->dt + 10e-3));
+        p->Vp_x = pos_p_x / p->dt;
+        p->Sp_x = p->Sp_x + pos_p_x;
+        p->Vp_y = dir * fabs(-p->Sp_y * dir - (p->cross_lines / 2.)) / p->dt;
+        p->Sp_y = -dir * p->cross_lines / 2.;
+        p->time_stop = 0;
+        p->at_crossing = 1;
+    } else if ((fabs(p->Sp_y) <= p->cross_lines / 2) + p->decision) {
+        if (p->time_stop != 0) {
+            p->Vp_x = 0.0;
+            p->Vp_y = 0.0;
+            p->time_stop = p->time_stop - 1;
+            p->t0 = p->t0 + p->dt;
+        } else if ((pyr_uniform(r, 0, 1) < 0.98) * p->choose) {
+            p->decision = 0;
+            double new_spy, new_vpy;
+            function_step(p, time, &new_spy, &new_vpy);
+            will_change_line(p, p->Sp_y, new_spy);
+            double distance_to_cross = ((double)p->max_lines - p->line_pos - 1) * p->cross * (double)(p->direction > 0);
+            distance_to_cross += (p->line_pos) * p->cross * (double)(p->direction < 0);
+            int new_choice;
+            if (p->change_line && (distance_to_cross > 0. && distance_to_cross < p->cross_lines)) {
+                new_choice = choix_pedestrian(e, p, cv);
+                if (new_choice && p->stop) p->stop = 0;
+            } else {
+                new_choice = 0;
+            }
+            if (p->stop) {
+                p->Vp_x = 0.0;
+                p->Vp_y = 0.0;
+                p->t0 = p->t0 + p->dt;
+                if (p->change_line) {
+                    p->time_before_crossing = p->time_before_crossing + p->dt;
+                    p->waiting_time = p->waiting_time + p->dt;
+                }
+            } else if (e->variant == V_SCALABLE && (p->need_to_stop) && p->Sp_y < p->cross_stop && pp_y > p->cross_stop) {
+                p->time_stop = (int)pyr_randint(r, 5, 35);
+                p->need_to_stop = 0;
+                if (!p->choose) {
+                    p->decision = 0;
+                    p->time_stop = 0;
+                    p->waiting_time = p->waiting_time + p->dt;
+                }
+                p->Vp_x = 0.0;
+                p->Vp_y = 0.0;
+                p->t0 = p->t0 + p->dt;
+            } else if ((!p->change_line) || (p->change_line && new_choice)) {
+                p->Sp_y = new_spy; p->Vp_y = new_vpy;
+                double nsx = p->Sp_x + p->Vp_y * p->ratio * p->dt, nvx = p->Vp_y * p->ratio;
+                p->Sp_x = nsx; p->Vp_x = nvx;
+                p->crossing_time = p->crossing_time + p->dt;
+                if (p->change_line && new_choice) apply_change_line(p, p->Sp_y, new_spy);
+            } else if (p->change_line && !new_choice) {
+                p->stop = 1;
+                double distance = fabs(dir * (p->cross_lines - distance_to_cross) - dir * p->cross_lines / 2. - p->Sp_y);
+                double pos_p_x = (p->Vp_x) * (distance) / fabs(p->Vp_y + 10e-3);
+                p->Vp_x = pos_p_x / p->dt;
+                p->Sp_x = p->Sp_x + pos_p_x;
+                p->Vp_y = dir * distance / p->dt;
+                p->Sp_y = dir * ((p->cross_lines - distance_to_cross) - p->cross_lines / 2.);
+            }
+            p->change_line = 0;
+        } else {
+            p->time_stop = (int)pyr_randint(r, 2, 5);
+            if (!p->choose) {
+                p->decision = 0;
+                p->time_stop = 0;
+                p->waiting_time = p->waiting_time + p->dt;
+            }
+            p->Vp_x = 0.0;
+            p->Vp_y = 0.0;
+            p->t0 = p->t0 + p->dt;
+        }
+    } else {
+        double nsx = p->Sp_x + p->init_speed[0] * p->dt, nvx = p->init_speed[0];
+        double nsy = p->Sp_y + p->init_speed[1] * p->dt, nvy = p->init_speed[1];
+        p->Sp_x = nsx; p->Vp_x = nvx;
+        p->Sp_y = nsy; p->Vp_y = nvy;
+    }
+}
+
+/* detection over the env's detection list (cars[], prev[]) -> out[n] */
+static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n, double *out) {
+    const int v = e->variant;
+    for (int i = 0; i < n; i++) {
+        Car *c = &cars[i];
+        int cond = is_in_front(p, c->line, 0);
+        if (v == V_SCALABLE) cond = cond && c->exist;
+        if (!cond) continue;
+        int ped_accident;
+        if (v == V_NAIF) {
+            p->worst_scenario_accident = worst_delta_l(e, p, c->Sc, c->Vc, c->line) < 0 ? 1 : 0;
+            ped_accident = (!p->accident) * (p->worst_scenario_accident);
+        } else {
+            ped_accident = (!p->accident) * (p->worst_scenario_accident);
+            p->worst_scenario_accident = worst_delta_l(e, p, c->Sc, c->Vc, c->line) < 0 ? 1 : 0;
+        }
+        if (ped_accident * (is_crossing_in_front(p, c->line, 0) * (prev[i] < p->Sp_x) * (c->Sc > p->Sp_x)))
+            p->accident = 1;
+        if (is_crossing_in_front(p, c->line, 0)) {
+            double dl;
+            if ((c->Vc) < 0.05) dl = (v == V_SCALABLE) ? 100. : 0.;
+            else dl = worst_delta_l(e, p, c->Sc, c->Vc, c->line) / (c->Vc);
+            double pa;
+            if (dl > 0) pa = -1. * exp(-4. * (dl));
+            else pa = (v == V_NAIF) ? -1. * dl - 1 : 1. * dl - 1;
+            c->possible_accident = pymin(c->possible_accident, pa);
+        }
+        if (v == V_NAIF) {
+            if (c->Sc < p->Sp_x)
+                c->Ts = pymax(p->waiting_time + 10. * p->crossing_time - c->time_braking + 1., c->Ts);
+        } else {
+            double clw = 0; /* sum([]) == 0 */
+            for (int k = 0; k < n; k++) {
+                if (cars[k].light > 0. && cars[k].Sc < p->Sp_x && (v != V_SCALABLE || cars[k].exist)) clw += 1.0;
+            }
+            if (c->Sc < p->Sp_x)
+                c->Ts = pymax((1. + clw) * p->waiting_time + 2. * p->crossing_time - c->time_braking + 1., c->Ts);
+        }
+        if (c->light < 0.0) {
+            double ne;
+            if (c->Ts < 0) ne = -1. * exp(4. * (c->Ts));
+            else ne = -1. * (1 + c->Ts);
+            c->error_scenario = pymin(ne, c->error_scenario);
+        }
+        if (c->light > 0.0) {
+            double ne;
+            if (p->Sp_x - c->Sc > 0) ne = -1. * exp(-4. * (p->Sp_x - c->Sc));
+            else ne = -1. * (1 + c->Sc - p->Sp_x);
+            c->error_scenario = pymin(ne, c->error_scenario);
+        }
+    }
+    double green = 0;
+    for (int k = 0; k < n; k++)
+        if (cars[k].light > 0. && (v != V_SCALABLE || cars[k].exist)) green += 1.0;
+    for (int i = 0; i < n; i++) {
+        Car *c = &cars[i];
+        double res = c->possible_accident + c->error_scenario;
+        double term = 0.5 * green * (double)(c->light < 0.) * (double)(c->Ts > 0);
+        if (v == V_COOP) res = res + term;
+        else if (v == V_4CARS || v == V_SCALABLE) res = res - term;
+        if (v == V_SCALABLE && !c->exist) res = 0.;
+        out[i] = res;
+    }
+}
+
+/* ---------------------------------------------------------------- car -- */
+
+static void car_init(OEnv *e, Car *c, double line, double offset_slot, int exist) {
+    memset(c, 0, sizeof(*c));
+    c->dt = e->dt;
+    c->cross = e->cross;
+    c->cross_lines = (double)e->nb_lines * e->cross;
+    c->line = line;
+    c->light = 0.;
+    c->Ac = 0.;
+    c->initial_speed = (double)e->speed_limit;
+    c->Vc = c->initial_speed;
+    c->possible_accident = 0.0;
+    c->error_scenario = 0.0;
+    c->Ts = (e->variant == V_SCALABLE) ? 0. : -10.;
+    const double(*pb)[4] = e->ped_b;
+    double mean_speed_ped = pb[0][1] + pb[1][1] / 2;
+    double min_speed_ped = pb[0][1], max_speed_ped = pb[1][1];
+    double finish_crosslines_time = (c->cross_lines * c->initial_speed) / (mean_speed_ped);
+    double low_car_range = (pb[0][3] * c->initial_speed) / min_speed_ped;
+    double high_car_range = (pb[1][3] * c->initial_speed) / max_speed_ped;
+    c->Sc = pyr_uniform(&e->rng, low_car_range - finish_crosslines_time, high_car_range);
+    if (e->variant == V_SCALABLE) c->Sc = c->Sc - 20.0 * offset_slot;
+    c->time_braking = -(c->Vc / (2.0 * e->car_b[0][0])) + 1.;
+    c->exist = exist;
+}
+
+static double car_follow_action(const OEnv *e, const Car *c, double lead_V, double lead_S) {
+    const double min_s = 2., T = 2.0, desired = 10.;
+    double speed_car = c->Vc;
+    double diff_dist = lead_S - c->Sc;
+    double delta_v = speed_car - lead_V;
+    double s = min_s + (speed_car * T) + (speed_car * delta_v) / (2 * sqrt(-e->car_b[0][0] * e->car_b[1][0]));
+    return e->car_b[1][0] * (1 - pow(speed_car / desired, 4.0) - pow(s / diff_dist, 2.0));
+}
+
+static void car_step(const OEnv *e, Car *c, double action, double light) {
+    double acc = pymin(pymax(action, e->car_b[0][0]), e->car_b[1][0]);
+    double sg;
+    if (c->Vc == 0.) {
+        sg = pymax(0., acc / fabs(acc));
+    } else if (acc > 0) {
+        sg = 1;
+    } else {
+        sg = pymax(pymin(-c->Vc / (c->dt * acc), 1.), 0.);
+    }
+    double final_acc = 0.0;
+    final_acc = final_acc + 1.0 * acc;
+    final_acc = final_acc + 0. * c->acc_hist[0];
+    final_acc = final_acc + 0. * c->acc_hist[1];
+    c->acc_hist[1] = c->acc_hist[0];
+    c->acc_hist[0] = acc;
+    final_acc = final_acc * sg;
+    double speed = c->Vc + c->dt * final_acc;
+    double pos = (final_acc * pow(c->dt, 2.0) / 2.0) + (c->Vc * c->dt) + (c->Sc);
+    c->Ac = final_acc; c->Vc = speed; c->Sc = pos; c->light = light;
+}
+
+static double car_reward(const Car *c) {
+    return -10. * pow(c->Vc - c->initial_speed, 2.0) / (c->initial_speed * c->initial_speed);
+}
+
+/* ---------------------------------------------------------------- env -- */
+
+OEnv *oracle_env_create(int variant, int nb_car, int nb_ped, int nb_lines, double dt, int max_episode,
+                        int sin_model, const double *car_b, const double *ped_b, const double *cross_b) {
+    OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
+    e->variant = variant;
+    e->nb_car = nb_car; e->nb_ped = nb_ped; e->nb_lines = nb_lines;
+    e->dt = dt; e->max_episode = max_episode; e->sin_model = sin_model;
+    for (int i = 0; i < 4; i++) e->car_b[i / 2][i % 2] = car_b[i];
+    for (int i = 0; i < 8; i++) e->ped_b[i / 4][i % 4] = ped_b[i];
+    e->cross_b[0] = cross_b[0]; e->cross_b[1] = cross_b[1];
+    e->nS = (variant == V_SCALABLE) ? 2 * nb_lines : nb_car;
+    if (e->nS > MAXC || nb_ped > MAXP) { free(e); return NULL; }
+    pyr_seed(&e->rng, 10); /* module import: random.seed(10) */
+    return e;
+}
+
+void oracle_env_destroy(OEnv *e) { free(e); }
+void oracle_env_seed(OEnv *e, uint64_t seed) { pyr_seed(&e->rng, seed); }
+uint64_t oracle_env_rng_words(const OEnv *e) { return e->rng.words; }
+void oracle_env_get_rng(const OEnv *e, uint32_t *mt, int32_t *mti) {
+    memcpy(mt, e->rng.mt, sizeof(e->rng.mt));
+    *mti = e->rng.mti;
+}
+
+int oracle_env_obs_dim(const OEnv *e) {
+    switch (e->variant) {
+    case V_4CARS: return 12 * e->nb_car + 3 + 9 * e->nb_ped;
+    case V_SCALABLE: return 7 * e->nS + 4 + 9 * e->nb_ped;
+    default: return 6 * e->nb_car + 3 + 9 * e->nb_ped;
+    }
+}
+
+static void car_data(const OEnv *e, const Car *c, double *o) {
+    int v = e->variant;
+    if (v == V_SCALABLE) {
+        if (!c->exist) {
+            o[0] = 0.; o[1] = 0.; o[2] = 10.; o[3] = -1000.; o[4] = 0; o[5] = c->line; o[6] = 0;
+        } else {
+            o[0] = c->Ac; o[1] = c->Vc; o[2] = c->initial_speed - c->Vc; o[3] = c->Sc; o[4] = c->light;
+            o[5] = c->line; o[6] = c->exist;
+        }
+        return;
+    }
+    if (v == V_COOP && !c->exist) {
+        o[0] = 0.; o[1] = 0.; o[2] = 0.; o[3] = 0.; o[4] = 0; o[5] = c->line;
+        return;
+    }
+    o[0] = c->Ac; o[1] = c->Vc; o[2] = c->initial_speed - c->Vc; o[3] = c->Sc; o[4] = c->light; o[5] = c->line;
+}
+
+/* flat observation in gym-sorted key order (car | car_follow | env | ped) */
+static void write_obs(OEnv *e, const CarView *pv, float *obs) {
+    int k = 0;
+    double tmp[9];
+    int cw = (e->variant == V_SCALABLE) ? 7 : 6;
+    for (int i = 0; i < e->nS; i++) {
+        car_data(e, &e->cars[i], tmp);
+        for (int j = 0; j < cw; j++) obs[k++] = (float)tmp[j];
+    }
+    if (e->variant == V_4CARS) {
+        for (int i = 0; i < e->nb_car; i++) {
+            car_data(e, &e->follow[i], tmp);
+            for (int j = 0; j < 6; j++) obs[k++] = (float)tmp[j];
+        }
+    }
+    obs[k++] = (float)(e->cross * (double)e->nb_lines / 2.);
+    obs[k++] = (float)e->ped_traffic;
+    if (e->variant == V_SCALABLE) obs[k++] = (float)e->car_traffic;
+    obs[k++] = (float)e->nb_lines;
+    for (int p = 0; p < e->nb_ped; p++) {
+        ped_get_data(e, &e->peds[p], pv, tmp);
+        for (int j = 0; j < 9; j++) obs[k++] = (float)tmp[j];
+    }
+}
+
+static void view_add(CarView *v, const Car *c) {
+    v->speed[v->n] = c->Vc; v->pos[v->n] = c->Sc; v->line[v->n] = c->line; v->light[v->n] = c->light;
+    v->n++;
+}
+
+void oracle_env_reset(OEnv *e, float *obs) {
+    PyRandom *r = &e->rng;
+    const int v = e->variant;
+    e->cross = pyr_uniform(r, e->cross_b[0], e->cross_b[1]);
+    e->speed_limit = 10;
+    for (int i = 0; i < e->nb_ped; i++) ped_init(e, &e->peds[i], 0, 0);
+    if (v == V_SCALABLE) {
+        for (int i = 0; i < e->nS; i++) car_init(e, &e->cars[i], (double)((i / 2) / 2), (double)((i / 2) % 2), 0);
+        e->car_traffic = (int)pyr_randint(r, 1, e->nb_car);
+        int nums[MAXC];
+        pyr_sample_range(r, e->nS, e->car_traffic, nums);
+        for (int k = 0; k < e->car_traffic; k++) {
+            int i = nums[k];
+            car_init(e, &e->cars[i], (double)((i / 2) / 2), (double)((i / 2) % 2), 1);
+        }
+    } else {
+        for (int i = 0; i < e->nb_car; i++) car_init(e, &e->cars[i], (double)(i % e->nb_lines), 0, 1);
+        if (v == V_4CARS)
+            for (int i = 0; i < e->nb_car; i++) car_init(e, &e->follow[i], e->cars[i].line, 0, 1);
+        e->car_traffic = e->nb_car;
+    }
+    e->ped_traffic = (int)pyr_randint(r, 1, e->nb_ped);
+    for (int i = 0; i < e->ped_traffic; i++) ped_init(e, &e->peds[i], 1, 1);
+    if (v == V_4CARS) {
+        for (int i = 0; i < e->nb_car; i++) { /* reset_car(speed_limit, Sc-15., 0, line) */
+            e->follow[i].Sc = e->cars[i].Sc - 15.;
+            e->follow[i].Vc = (double)e->speed_limit;
+            e->follow[i].light = 0;
+            e->follow[i].line = e->cars[i].line;
+        }
+    }
+    CarView cv; /* reset observation sees every AV slot (:869-876 / :922-929) */
+    cv.n = 0;
+    for (int i = 0; i < e->nS; i++) view_add(&cv, &e->cars[i]);
+    write_obs(e, &cv, obs);
+    e->time = 0.0;
+    for (int i = 0; i < MAXC; i++) e->reward_light[i] = 0.0;
+    e->episode_length = (double)(e->max_episode - 1) * e->dt;
+}
+
+int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards, double *reward_light) {
+    const int v = e->variant;
+    const int nS = e->nS;
+    double prev[MAXC];
+    for (int i = 0; i < nS; i++) prev[i] = e->cars[i].Sc;
+    for (int i = 0; i < nS; i++) {
+        Car *c = &e->cars[i];
+        double a = actions[i];
+        if (v == V_SCALABLE) {
+            double idm = 2.;
+            if (i % 2 == 1 && e->cars[i - 1].exist && c->exist) {
+                const Car *l = &e->cars[i - 1];
+                idm = car_follow_action(e, c, l->exist ? l->Vc : 0., l->exist ? l->Sc : -1000.);
+            }
+            a = pymin(idm, a);
+        }
+        car_step(e, c, a, actions[i + nS]);
+    }
+    if (v == V_4CARS) {
+        for (int i = 0; i < e->nb_car; i++) {
+            const Car *l = &e->cars[i];
+            double a = car_follow_action(e, &e->follow[i], l->Vc, l->Sc);
+            car_step(e, &e->follow[i], a, l->light);
+        }
+    }
+    CarView cv;
+    cv.n = 0;
+    for (int i = 0; i < nS; i++)
+        if (v != V_SCALABLE || e->cars[i].exist) view_add(&cv, &e->cars[i]);
+    if (v == V_4CARS)
+        for (int i = 0; i < e->nb_car; i++) view_add(&cv, &e->follow[i]);
+    for (int p = 0; p < e->nb_ped; p++) ped_step(e, &e->peds[p], e->time, &cv);
+
+    double dangers[MAXC], det[MAXC];
+    for (int i = 0; i < nS; i++) dangers[i] = 0.;
+    for (int p = 0; p < e->nb_ped; p++) {
+        Ped *pd = &e->peds[p];
+        ped_detection(e, pd, e->cars, prev, nS, det);
+        if (pd->is_crossing && nS && (v != V_SCALABLE || pd->exist))
+            for (int i = 0; i < nS; i++) dangers[i] += det[i];
+    }
+    for (int i = 0; i < nS; i++) e->reward_light[i] = dangers[i];
+    for (int i = 0; i < nS; i++) {
+        Car *c = &e->cars[i];
+        double rew = car_reward(c);
+        if (c->light > 0.0) {
+            int have = 0;
+            double mn = 0.;
+            for (int p = 0; p < e->nb_ped; p++) {
+                Ped *pd = &e->peds[p];
+                if (!pd->exist) continue;
+                double w = new_reward_wait_safety(e, pd, c->Vc, c->Sc, c->line);
+                if (!have) { mn = w; have = 1; }
+                else if (w < mn) mn = w;
+            }
+            if (have) rew += mn;
+        }
+        rewards[i] = rew;
+    }
+    write_obs(e, &cv, obs);
+    int done = (e->time >= e->episode_length) || (e->ped_traffic <= 0);
+    e->time = e->time + e->dt;
+    for (int i = 0; i < nS; i++) reward_light[i] = e->reward_light[i];
+    return done;
+}
+
+/* Internal state dump for fixture cross-checks: per ped 20 doubles, per car 8. */
+int oracle_env_dump(const OEnv *e, double *out) {
+    int k = 0;
+    for (int p = 0; p < e->nb_ped; p++) {
+        const Ped *d = &e->peds[p];
+        double f[20] = {d->Sp_x, d->Sp_y, d->Vp_x, d->Vp_y, (double)d->decision, (double)d->at_crossing,
+                        (double)d->ped_left, (double)d->ped_in_cross, (double)d->accident, (double)d->time_stop,
+                        (double)d->stop, d->line_pos, d->waiting_time, d->crossing_time, d->worst_dl, d->delta,
+                        d->t0, (double)d->need_to_stop, (double)d->direction, (double)d->follow_rule};
+        for (int j = 0; j < 20; j++) out[k++] = f[j];
+    }
+    for (int i = 0; i < e->nS; i++) {
+        const Car *c = &e->cars[i];
+        double f[8] = {c->Ac, c->Vc, c->Sc, c->light, c->possible_accident, c->error_scenario, c->Ts, (double)c->exist};
+        for (int j = 0; j < 8; j++) out[k++] = f[j];
+    }
+    return k;
+}
