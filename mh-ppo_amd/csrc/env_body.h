@@ -1,0 +1,333 @@
+// env_body.h — per-env reset/step/state bodies (host+device).  The HIP
+// kernels in mhppo_env.hip launch one lane per env over these; tools/hostsim.cpp
+// runs the same source on the CPU.
+#pragma once
+#include <string.h>
+
+#include "../../include/mhppo.h"
+#include "env_dev.h"
+
+namespace mhppo {
+constexpr int MAXS = 16;  // AV slots per env (scalable 2*nb_lines, coop nb_car)
+
+// ----------------------------------------------------------------- reset
+template <int V>
+MHPPO_HD void ped_init(Env<V> &E, Ped &q, int is_crossing, int exist) {
+  Rng &r = E.rng;
+  const Cfg &c = E.c;
+  q = Ped{};
+  q.wdl = 0.0;
+  q.fl = 0;
+  q.set(F_ISCROSS, is_crossing);
+  (void)r.randint(0, 20);  // time_to_remove (never read)
+  q.set(F_FOLLOW, r.randint(0, 9) < (V == V_NAIF ? 10 : 3));
+  q.set(F_EXIST, exist);
+  q.dir = 2 * r.randint(0, 1) - 1;
+  q.lpos = (double)(c.nb_lines * (q.dir < 0) - 1 * (q.dir > 0));
+  q.ivx = r.uniform(c.pb[0][0], c.pb[1][0]);
+  q.ivy = r.uniform(c.pb[0][1], c.pb[1][1]) * (double)q.dir;
+  double px = r.uniform(c.pb[0][2], c.pb[1][2]);
+  double py = (r.uniform(c.pb[0][3], c.pb[1][3]) - E.cl / 2.) * (double)q.dir;
+  q.ratio = 0.0;
+  if (!exist) {
+    q.ivx = 0.;
+    q.ivy = 0.;
+    if (V == V_4CARS || V == V_NAIF) px = c.pb[0][2];
+    py = c.pb[0][3] * (double)q.dir;
+  } else if (!is_crossing) {
+    q.ivx = 0.;
+    q.ivy = 0.;
+    q.dir = 0;
+  } else {
+    q.ratio = q.ivx / q.ivy;
+  }
+  q.Vx = q.ivx;
+  q.Vy = q.ivy;
+  q.Sx = px;
+  q.Sy = py;
+  q.tstop = 0;
+  q.t0 = 0.0;
+  q.set(F_GENDER, r.randint(0, 1) == 1);
+  int age = r.randint(0, 2);
+  q.fl = (q.fl & ~F_AGE_MASK) | ((uint32_t)age << F_AGE_SHIFT);
+  (void)CG_score(E, q, E.cross);  // self.CG: draws, never read
+  q.delta = 0.0;
+  q.cstop = 0.0;
+  if (V == V_COOP) {
+    q.set(F_NEEDSTOP, true);
+    q.cstop = r.uniform(-E.cl / 2 + 0.2, E.cl / 2 - 0.2);
+  } else if (V == V_SCALABLE) {
+    q.set(F_NEEDSTOP, r.uniform(0, 1) < 0.5);
+    q.cstop = r.uniform(-E.cl / 2 + 0.2, E.cl / 2 - 0.2);
+  }
+  q.A = q.B = q.W = 0.0;
+  if (c.sin_model && is_crossing) {
+    q.set(F_SIN, true);
+    double abs_speed = fabs(q.ivy);
+    double T = E.cl / (abs_speed + 10e-3);
+    int check = ((abs_speed * PI) / 2.0 <= 2.5);
+    q.A = (double)check * PI * abs_speed / 2.0 + (double)(!check) * (2.5 - abs_speed) / (1.0 - (2.0 / PI));
+    q.B = (double)(!check) * (2.5 - q.A);
+    q.W = PI / T;
+  }
+}
+
+template <int V>
+MHPPO_HD void car_init(Env<V> &E, int s, double line, double offset, int exist) {
+  const Cfg &c = E.c;
+  double finish = (E.cl * 10.0) / (c.mean_speed_ped);
+  double Sc = E.rng.uniform(c.car_low - finish, c.car_high);
+  if (V == V_SCALABLE) Sc = Sc - 20.0 * offset;
+  E.car(C_AC, s) = 0.;
+  E.car(C_VC, s) = 10.0;
+  E.car(C_SC, s) = Sc;
+  E.car(C_LIGHT, s) = 0.;
+  E.car(C_PA, s) = 0.0;
+  E.car(C_ES, s) = 0.0;
+  E.car(C_TS, s) = (V == V_SCALABLE) ? 0. : -10.;
+  E.car(C_H0, s) = 0.;
+  E.car(C_H1, s) = 0.;
+  E.car(C_LINE, s) = line;
+  E.car(C_EXIST, s) = exist ? 1.0 : 0.0;
+}
+
+// car.get_data for the flat obs (coop :609-612, scalable :652-655)
+template <int V>
+MHPPO_HD int write_car_obs(const Env<V> &E, int s, float *o) {
+  if (V == V_SCALABLE) {
+    if (E.car(C_EXIST, s) == 0.0) {
+      o[0] = 0.f; o[1] = 0.f; o[2] = 10.f; o[3] = -1000.f; o[4] = 0.f; o[5] = (float)E.car(C_LINE, s); o[6] = 0.f;
+    } else {
+      double Vc = E.car(C_VC, s);
+      o[0] = (float)E.car(C_AC, s); o[1] = (float)Vc; o[2] = (float)(10.0 - Vc); o[3] = (float)E.car(C_SC, s);
+      o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.car(C_LINE, s); o[6] = 1.f;
+    }
+    return 7;
+  }
+  double Vc = E.car(C_VC, s);
+  o[0] = (float)E.car(C_AC, s); o[1] = (float)Vc; o[2] = (float)(10.0 - Vc); o[3] = (float)E.car(C_SC, s);
+  o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.car(C_LINE, s);
+  return 6;
+}
+
+// flat obs (gym-sorted car|car_follow|env|ped); ped.get_data runs even without
+// an obs buffer because it advances the running-min `delta` (:441).
+template <int V>
+MHPPO_HD void env_observe(Env<V> &E, int mode, float *obs) {
+  const Cfg &c = E.c;
+  float *o = obs ? obs + (size_t)E.e * c.obs_dim : nullptr;
+  float tmp[8];
+  int k = 0;
+  if (o) {
+    for (int s = 0; s < c.nC; s++) {
+      int w = write_car_obs(E, s, tmp);
+      for (int j = 0; j < w; j++) o[k++] = tmp[j];
+    }
+    o[k++] = (float)(E.cross * (double)c.nb_lines / 2.);
+    o[k++] = (float)E.b.envi[EI_PEDTRAF * c.N + E.e];
+    if (V == V_SCALABLE) o[k++] = (float)E.b.envi[EI_CARTRAF * c.N + E.e];
+    o[k++] = (float)c.nb_lines;
+  }
+  for (int p = 0; p < c.P; p++) {
+    Ped q = load_ped(E, p);
+    double d[9];
+    ped_get_data(E, q, mode, d);
+    E.pedf(P_DELTA, p) = q.delta;
+    if (o)
+      for (int j = 0; j < 9; j++) o[k++] = (float)d[j];
+  }
+}
+
+template <int V>
+MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
+  // cross first: it sizes everything else (:844)
+  Env<V> E(c, b, e);
+  E.cross = E.rng.uniform(c.xb0, c.xb1);
+  E.cl = (double)c.nb_lines * E.cross;
+  b.envd[E_CROSS * c.N + e] = E.cross;
+  for (int p = 0; p < c.P; p++) {
+    Ped q;
+    ped_init(E, q, 0, 0);
+    store_ped(E, p, q, false);
+  }
+  int car_traffic = c.nb_car;
+  if (V == V_SCALABLE) {
+    for (int i = 0; i < c.nS; i++) car_init(E, i, (double)((i / 2) / 2), (double)((i / 2) % 2), 0);
+    car_traffic = E.rng.randint(1, c.nb_car);
+    // random.sample(range(S), k) (pool algorithm) draws every index first; the
+    // chosen cars are then re-built in sample order (:903-906)
+    uint64_t pool = 0, order = 0;
+    for (int i = 0; i < c.nS; i++) pool |= (uint64_t)i << (4 * i);
+    for (int k = 0; k < car_traffic; k++) {
+      int j = (int)E.rng.randbelow((uint32_t)(c.nS - k));
+      uint64_t pick = (pool >> (4 * j)) & 15u;
+      uint64_t last = (pool >> (4 * (c.nS - k - 1))) & 15u;
+      pool = (pool & ~(15ull << (4 * j))) | (last << (4 * j));
+      order |= pick << (4 * k);
+    }
+    for (int k = 0; k < car_traffic; k++) {
+      int pick = (int)((order >> (4 * k)) & 15u);
+      car_init(E, pick, (double)((pick / 2) / 2), (double)((pick / 2) % 2), 1);
+    }
+  } else {
+    for (int i = 0; i < c.nb_car; i++) car_init(E, i, (double)(i % c.nb_lines), 0, 1);
+    if (V == V_4CARS)
+      for (int i = 0; i < c.nb_car; i++) car_init(E, c.nS + i, E.car(C_LINE, i), 0, 1);
+  }
+  b.envi[EI_CARTRAF * c.N + e] = car_traffic;
+  int ped_traffic = E.rng.randint(1, c.nb_ped);
+  b.envi[EI_PEDTRAF * c.N + e] = ped_traffic;
+  for (int p = 0; p < ped_traffic; p++) {
+    Ped q;
+    ped_init(E, q, 1, 1);
+    store_ped(E, p, q, false);
+  }
+  if (V == V_4CARS) {
+    for (int i = 0; i < c.nb_car; i++) {  // reset_car(speed_limit, Sc - 15., 0, line) (:878-879)
+      E.car(C_SC, c.nS + i) = E.car(C_SC, i) - 15.;
+      E.car(C_VC, c.nS + i) = 10.0;
+      E.car(C_LIGHT, c.nS + i) = 0.;
+      E.car(C_LINE, c.nS + i) = E.car(C_LINE, i);
+    }
+  }
+  env_observe(E, 0, obs);
+  b.envd[E_TIME * c.N + e] = 0.0;
+  E.save_rng();
+}
+
+// ------------------------------------------------------------------ step
+template <int V>
+MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *actions, float *obs, double *rew,
+                           double *rlight, uint8_t *done) {
+  Env<V> E(c, b, e);
+  const int nS = c.nS;
+  const double *act = actions + (size_t)e * 2 * nS;
+  double time = b.envd[E_TIME * c.N + e];
+  double prev[MAXS];
+  for (int i = 0; i < nS; i++) prev[i] = E.car(C_SC, i);
+  for (int i = 0; i < nS; i++) {
+    double a = act[i];
+    if (V == V_SCALABLE) {
+      double idm = 2.;
+      if (i % 2 == 1 && E.car(C_EXIST, i - 1) != 0.0 && E.car(C_EXIST, i) != 0.0)
+        idm = car_follow_action(E, i, E.car(C_VC, i - 1), E.car(C_SC, i - 1));
+      a = pymin(idm, a);
+    }
+    car_step(E, i, a, act[i + nS]);
+  }
+  if (V == V_4CARS)
+    for (int i = 0; i < c.nb_car; i++) {
+      double a = car_follow_action(E, nS + i, E.car(C_VC, i), E.car(C_SC, i));
+      car_step(E, nS + i, a, E.car(C_LIGHT, i));
+    }
+  for (int p = 0; p < c.P; p++) {
+    Ped q = load_ped(E, p);
+    ped_step(E, q, time);
+    store_ped(E, p, q, true);
+  }
+  double acc[MAXS];
+  for (int i = 0; i < nS; i++) acc[i] = 0.;
+  for (int p = 0; p < c.P; p++) {
+    Ped q = load_ped(E, p);
+    bool add = q.has(F_ISCROSS) && (V != V_SCALABLE || q.has(F_EXIST));
+    ped_detection<V, MAXS>(E, q, prev, acc, add);
+    E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
+  }
+  double *rl = rlight + (size_t)e * nS;
+  double *rw = rew + (size_t)e * nS;
+  for (int i = 0; i < nS; i++) {
+    if (rlight) rl[i] = acc[i];
+    double Vc = E.car(C_VC, i);
+    double r = car_reward(Vc);
+    if (E.car(C_LIGHT, i) > 0.0) {
+      bool have = false;
+      double mn = 0.;
+      for (int p = 0; p < c.P; p++) {
+        uint32_t fl = E.pflag(p);
+        if (!(fl & F_EXIST)) continue;
+        Ped q = load_ped(E, p);
+        double w = new_reward_wait_safety(E, q, Vc, E.car(C_SC, i), E.car(C_LINE, i));
+        E.pedf(P_WDL, p) = q.wdl;
+        if (!have) { mn = w; have = true; }
+        else if (w < mn) mn = w;
+      }
+      if (have) r += mn;
+    }
+    if (rew) rw[i] = r;
+  }
+  env_observe(E, 1, obs);
+  int d = (time >= c.ep_len) || (b.envi[EI_PEDTRAF * c.N + e] <= 0);
+  if (done) done[e] = (uint8_t)d;
+  b.envd[E_TIME * c.N + e] = time + c.dt;
+  E.save_rng();
+}
+
+// ------------------------------------------------------------- seeding
+MHPPO_HD inline void env_seed_one(const Cfg &c, const Bufs &b, int e) {
+  rng_seed(b.mt + (size_t)e * 624, c.seed_base + c.env_off + (uint64_t)e);
+  b.envi[EI_MTI * c.N + e] = 624;
+  b.envd[E_CROSS * c.N + e] = 0.0;
+  b.envd[E_TIME * c.N + e] = 0.0;
+}
+
+// ------------------------------------------------------------- state dump
+// [peds 20P][AV cars 8 nS][followers 8 (nC-nS)][cross, time, ped_traffic, car_traffic]
+template <int V>
+MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int dim) {
+  Env<V> E(c, b, e);
+  double *o = out + (size_t)e * dim;
+  int k = 0;
+  for (int p = 0; p < c.P; p++) {
+    Ped q = load_ped(E, p);
+    double f[20] = {q.Sx, q.Sy, q.Vx, q.Vy, (double)q.has(F_DECISION), (double)q.has(F_ATCROSS),
+                    (double)q.has(F_LEFT), (double)q.has(F_INCROSS), (double)q.has(F_ACCIDENT), (double)q.tstop,
+                    (double)q.has(F_STOP), q.lpos, q.wt, q.ct, q.wdl, q.delta, q.t0,
+                    (double)q.has(F_NEEDSTOP), (double)q.dir, (double)q.has(F_FOLLOW)};
+    for (int j = 0; j < 20; j++) o[k++] = f[j];
+  }
+  for (int s = 0; s < c.nC; s++) {
+    double f[8] = {E.car(C_AC, s), E.car(C_VC, s), E.car(C_SC, s), E.car(C_LIGHT, s),
+                   E.car(C_PA, s), E.car(C_ES, s), E.car(C_TS, s), E.car(C_EXIST, s)};
+    for (int j = 0; j < 8; j++) o[k++] = f[j];
+  }
+  o[k++] = E.cross;
+  o[k++] = b.envd[E_TIME * c.N + e];
+  o[k++] = (double)b.envi[EI_PEDTRAF * c.N + e];
+  o[k++] = (double)b.envi[EI_CARTRAF * c.N + e];
+}
+
+
+// host: mhppo_env_cfg -> Cfg (constants that are transcendental functions of the
+// config are evaluated here, with glibc, exactly as the reference does)
+inline void build_cfg(const mhppo_env_cfg &cfg_, Cfg &c) {
+  const mhppo_env_cfg *cfg = &cfg_;
+  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : cfg->nb_car;
+  memset(&c, 0, sizeof(c));
+  c.variant = cfg->variant;
+  c.N = cfg->n_envs;
+  c.nb_car = cfg->nb_car;
+  c.nb_ped = cfg->nb_ped;
+  c.nb_lines = cfg->nb_lines;
+  c.nS = nS;
+  c.nC = cfg->variant == V_4CARS ? 2 * nS : nS;
+  c.P = cfg->nb_ped;
+  c.max_episode = cfg->max_episode;
+  c.sin_model = cfg->sin_model;
+  c.obs_dim = cfg->variant == V_4CARS ? 12 * nS + 3 + 9 * c.P
+                                      : (cfg->variant == V_SCALABLE ? 7 * nS + 4 + 9 * c.P : 6 * nS + 3 + 9 * c.P);
+  c.dt = cfg->dt;
+  c.dt2 = pow(cfg->dt, 2.0);  // math.pow(self.dt, 2.0) (:604), glibc on the host
+  c.b00 = cfg->car_b[0];
+  c.b10 = cfg->car_b[2];
+  for (int i = 0; i < 8; i++) c.pb[i / 4][i % 4] = cfg->ped_b[i];
+  c.xb0 = cfg->cross_b[0];
+  c.xb1 = cfg->cross_b[1];
+  c.idm_den = 2 * sqrt(-c.b00 * c.b10);                 // (:619)
+  c.ep_len = (double)(cfg->max_episode - 1) * cfg->dt;  // episode_length (:892)
+  c.mean_speed_ped = c.pb[0][1] + c.pb[1][1] / 2;       // (:549)
+  c.car_low = (c.pb[0][3] * 10.0) / c.pb[0][1];         // low_car_range (:557)
+  c.car_high = (c.pb[1][3] * 10.0) / c.pb[1][1];        // high_car_range (:558)
+  c.seed_base = cfg->seed_base;
+  c.env_off = cfg->env_id_offset;
+}
+}  // namespace mhppo

@@ -1,0 +1,621 @@
+// env_dev.h — device-side crosswalk env for gfx950: one env per lane.
+//
+// State lives in HBM as structure-of-arrays, field-major with the env index
+// fastest ([field][slot][N]), so every per-lane access of a wave is one
+// coalesced 512-B transaction.  Each env draws from its own CPython-compatible
+// MT19937 stream (state [N][624] u32 + cursor), so trajectories are the
+// reference's on `random.seed(seed_base + env_id)` and invariant to how envs
+// are sharded over GPUs.
+//
+// Semantics follow the reference statement by statement (file:line under
+// /root/reference/Environments, coop file unless noted):
+//   pedestrian.__init__ :15-103, choix_pedestrian :138-173 (naif :129-174,
+//   4cars no shuffle), detection :175-259 (scalable :176-264, naif :176-215),
+//   ped.step :292-401 (+ scalable mid-cross stop :371-380), CG_score :403-412,
+//   get_data/is_in_front/is_crossing_in_front/new_reward_wait_safety/
+//   delta_l* :433-511, car :515-622, IDM follow_action scalable :604-624,
+//   car_follower 4cars :13-129, env.step :745-832, env.reset :838-893.
+// Python's two-argument min/max keep the FIRST argument unless the second is
+// strictly smaller/greater; pymin/pymax reproduce that (NaN included).
+// Built with -ffp-contract=off: no FMA contraction, Python's rounding order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+// Every env routine is __host__ __device__: the kernels run it on gfx950 and
+// tools/hostsim.cpp runs the identical source on the CPU for debugging.
+#define MHPPO_HD __host__ __device__
+
+namespace mhppo {
+
+enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3 };
+
+// car fields (double) [C_NF][nC][N]
+enum { C_AC, C_VC, C_SC, C_LIGHT, C_PA, C_ES, C_TS, C_H0, C_H1, C_LINE, C_EXIST, C_NF };
+// ped fields (double) [P_NF][P][N]
+enum { P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS, P_IVX, P_IVY, P_RATIO,
+       P_CSTOP, P_A, P_B, P_W, P_NF };
+// ped flag word bits [P][N] (u32)
+enum : uint32_t {
+  F_DECISION = 1u << 0, F_ATCROSS = 1u << 1, F_LEFT = 1u << 2, F_INCROSS = 1u << 3,
+  F_ACCIDENT = 1u << 4, F_STOP = 1u << 5, F_WSA = 1u << 6, F_NEEDSTOP = 1u << 7,
+  F_EXIST = 1u << 8, F_ISCROSS = 1u << 9, F_FOLLOW = 1u << 10, F_DIRNEG = 1u << 11,
+  F_DIRPOS = 1u << 12, F_GENDER = 1u << 13, F_SIN = 1u << 14,
+  F_AGE_SHIFT = 16, F_AGE_MASK = 3u << 16,
+  F_TSTOP_SHIFT = 20, F_TSTOP_MASK = 0xFFu << 20,
+};
+// env scalars
+enum { E_CROSS, E_TIME, E_ND };
+enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_NI };
+
+struct Cfg {
+  int variant, N, nb_car, nb_ped, nb_lines, nS, nC, P, max_episode, sin_model, obs_dim, pad;
+  double dt, dt2, b00, b10, pb[2][4], xb0, xb1, idm_den, ep_len;
+  // car.__init__ position bounds (:549-560): low/high_car_range, mean_speed_ped (host-computed)
+  double car_low, car_high, mean_speed_ped;
+  uint64_t seed_base, env_off;
+};
+
+struct Bufs {
+  double *car;    // [C_NF][nC][N]
+  double *ped;    // [P_NF][P][N]
+  uint32_t *pfl;  // [P][N]
+  double *envd;   // [E_ND][N]
+  int32_t *envi;  // [EI_NI][N]
+  uint32_t *mt;   // [N][624]
+};
+
+MHPPO_HD __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
+MHPPO_HD __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
+
+static constexpr double PI = 0x1.921fb54442d18p+1;
+static constexpr double NV_MAGICCONST = 0x1.b72cd3f331398p+0;  // 4*exp(-0.5)/sqrt(2.0)
+
+// ------------------------------------------------------------ CPython random
+struct Rng {
+  uint32_t *mt;  // this env's 624 words
+  int mti;
+
+  MHPPO_HD uint32_t genrand() {
+    if (mti >= 624) {
+      uint32_t y;
+      int kk;
+      for (kk = 0; kk < 624 - 397; kk++) {
+        y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+        mt[kk] = mt[kk + 397] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      for (; kk < 623; kk++) {
+        y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+        mt[kk] = mt[kk - 227] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+      mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      mti = 0;
+    }
+    uint32_t y = mt[mti++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  MHPPO_HD double random() {
+    uint32_t a = genrand() >> 5, b = genrand() >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+  MHPPO_HD uint32_t randbelow(uint32_t n) {
+    if (!n) return 0;
+    int k = 0;
+    for (uint32_t t = n; t; t >>= 1) k++;
+    uint32_t v = genrand() >> (32 - k);
+    while (v >= n) v = genrand() >> (32 - k);
+    return v;
+  }
+  MHPPO_HD int randint(int a, int b) { return a + (int)randbelow((uint32_t)(b - a + 1)); }
+  MHPPO_HD double uniform(double a, double b) { return a + (b - a) * random(); }
+  MHPPO_HD double normalvariate(double mu, double sigma) {
+    double z;
+    for (;;) {
+      double u1 = random();
+      double u2 = 1.0 - random();
+      z = NV_MAGICCONST * (u1 - 0.5) / u2;
+      double zz = z * z / 4.0;
+      if (zz <= -log(u2)) break;
+    }
+    return mu + z * sigma;
+  }
+};
+
+// init_by_array([seed lo, seed hi]) exactly as CPython's random.seed(int)
+MHPPO_HD inline void rng_seed(uint32_t *mt, uint64_t seed) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  int klen = key[1] ? 2 : 1;
+  mt[0] = 19650218u;
+  for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+  int i = 1, j = 0;
+  for (int k = 624; k; k--) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+    i++; j++;
+    if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    if (j >= klen) j = 0;
+  }
+  for (int k = 623; k; k--) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+    i++;
+    if (i >= 624) { mt[0] = mt[623]; i = 1; }
+  }
+  mt[0] = 0x80000000u;
+}
+
+// CPython float floor division (Objects/floatobject.c _float_div_mod)
+MHPPO_HD inline double py_floordiv(double vx, double wx) {
+  double mod = fmod(vx, wx);
+  double div = (vx - mod) / wx;
+  if (mod) {
+    if ((wx < 0) != (mod < 0)) { mod += wx; div -= 1.0; }
+  }
+  double fl;
+  if (div) {
+    fl = floor(div);
+    if (div - fl > 0.5) fl += 1.0;
+  } else {
+    fl = copysign(0.0, vx / wx);
+  }
+  return fl;
+}
+
+// ---------------------------------------------------------------- env view
+// One lane's view of its env.  Car/ped fields are read and written in place
+// in HBM (coalesced across the wave); the pedestrian being stepped is staged
+// in registers (struct Ped) for the duration of its update.
+template <int V>
+struct Env {
+  const Cfg &c;
+  const Bufs &b;
+  int e;
+  Rng rng;
+  double cross, cl;  // crosswalk lane width, cross_lines = nb_lines * cross
+
+  MHPPO_HD Env(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
+    rng.mt = b.mt + (size_t)e * 624;
+    rng.mti = b.envi[EI_MTI * c.N + e];
+    cross = b.envd[E_CROSS * c.N + e];
+    cl = (double)c.nb_lines * cross;
+  }
+  MHPPO_HD void save_rng() { b.envi[EI_MTI * c.N + e] = rng.mti; }
+
+  MHPPO_HD double &car(int f, int s) const { return b.car[((size_t)f * c.nC + s) * c.N + e]; }
+  MHPPO_HD double &pedf(int f, int p) const { return b.ped[((size_t)f * c.P + p) * c.N + e]; }
+  MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[(size_t)p * c.N + e]; }
+};
+
+struct Ped {
+  double Sx, Sy, Vx, Vy, t0, wt, ct, wdl, delta, lpos, ivx, ivy, ratio, cstop, A, B, W;
+  uint32_t fl;
+  int dir, tstop;
+  MHPPO_HD bool has(uint32_t f) const { return (fl & f) != 0; }
+  MHPPO_HD void set(uint32_t f, bool v) { fl = v ? (fl | f) : (fl & ~f); }
+};
+
+template <int V>
+MHPPO_HD inline Ped load_ped(const Env<V> &E, int p) {
+  Ped q;
+  q.Sx = E.pedf(P_SX, p); q.Sy = E.pedf(P_SY, p); q.Vx = E.pedf(P_VX, p); q.Vy = E.pedf(P_VY, p);
+  q.t0 = E.pedf(P_T0, p); q.wt = E.pedf(P_WT, p); q.ct = E.pedf(P_CT, p); q.wdl = E.pedf(P_WDL, p);
+  q.delta = E.pedf(P_DELTA, p); q.lpos = E.pedf(P_LPOS, p); q.ivx = E.pedf(P_IVX, p);
+  q.ivy = E.pedf(P_IVY, p); q.ratio = E.pedf(P_RATIO, p); q.cstop = E.pedf(P_CSTOP, p);
+  q.A = E.pedf(P_A, p); q.B = E.pedf(P_B, p); q.W = E.pedf(P_W, p);
+  q.fl = E.pflag(p);
+  q.dir = (q.fl & F_DIRNEG) ? -1 : ((q.fl & F_DIRPOS) ? 1 : 0);
+  q.tstop = (int)((q.fl & F_TSTOP_MASK) >> F_TSTOP_SHIFT);
+  return q;
+}
+
+template <int V>
+MHPPO_HD inline void store_ped(const Env<V> &E, int p, Ped &q, bool dyn_only) {
+  E.pedf(P_SX, p) = q.Sx; E.pedf(P_SY, p) = q.Sy; E.pedf(P_VX, p) = q.Vx; E.pedf(P_VY, p) = q.Vy;
+  E.pedf(P_T0, p) = q.t0; E.pedf(P_WT, p) = q.wt; E.pedf(P_CT, p) = q.ct; E.pedf(P_WDL, p) = q.wdl;
+  E.pedf(P_DELTA, p) = q.delta; E.pedf(P_LPOS, p) = q.lpos;
+  if (!dyn_only) {
+    E.pedf(P_IVX, p) = q.ivx; E.pedf(P_IVY, p) = q.ivy; E.pedf(P_RATIO, p) = q.ratio;
+    E.pedf(P_CSTOP, p) = q.cstop; E.pedf(P_A, p) = q.A; E.pedf(P_B, p) = q.B; E.pedf(P_W, p) = q.W;
+  }
+  uint32_t fl = q.fl & ~(F_TSTOP_MASK | F_DIRNEG | F_DIRPOS);
+  fl |= ((uint32_t)q.tstop << F_TSTOP_SHIFT) & F_TSTOP_MASK;
+  if (q.dir < 0) fl |= F_DIRNEG;
+  if (q.dir > 0) fl |= F_DIRPOS;
+  E.pflag(p) = fl;
+}
+
+// ------------------------------------------------------- pedestrian geometry
+template <int V>
+MHPPO_HD inline bool is_in_front(const Env<V> &E, const Ped &q, double car_line, double next_line) {
+  double line_1 = (-E.cl / 2) + E.cross * (car_line - 0.5 * next_line + 1);
+  double line_2 = (E.cl / 2) - E.cross * ((double)E.c.nb_lines - 0.5 * next_line - car_line);
+  if (q.dir == -1) return q.Sy >= line_2 - 0.001;
+  return q.Sy <= line_1 + 0.001;
+}
+
+template <int V>
+MHPPO_HD inline bool is_crossing_in_front(const Env<V> &E, const Ped &q, double car_line, double prev_line) {
+  double line_1 = (-E.cl / 2) + E.cross * (car_line - prev_line);
+  double line_2 = (E.cl / 2) - E.cross * ((double)E.c.nb_lines - car_line - 1 - prev_line);
+  if (q.dir == -1) return q.Sy < line_2;
+  return q.Sy > line_1;
+}
+
+// which car slots the pedestrians see: mode 0 = reset observation (all AV slots),
+// mode 1 = step (existing AVs [+ followers for 4cars])
+template <int V>
+MHPPO_HD inline bool in_view(const Env<V> &E, int s, int mode) {
+  if (V == V_4CARS) return mode == 1 || s < E.c.nS;
+  if (V == V_SCALABLE) return mode == 0 || E.car(C_EXIST, s) != 0.0;
+  return true;
+}
+
+template <int V>
+MHPPO_HD inline double CG_score(Env<V> &E, const Ped &q, double crossing_size) {
+  if (!q.has(F_ISCROSS)) return 0.;
+  const double fem = 0.0369, child = -0.0355, midage = -0.0221, old = -0.1810;
+  const double alpha = 0.09, sigma = 0.09;
+  int age = (int)((q.fl & F_AGE_MASK) >> F_AGE_SHIFT);
+  double gamma = log10(crossing_size / fabs(q.ivy + 10e-3));
+  double log_val = alpha + gamma + fem * (double)(q.has(F_GENDER)) + child * (double)(age == 0) +
+                   midage * (double)(age == 1) + old * (double)(age == 2);
+  log_val = log_val + E.rng.normalvariate(0.0, sigma);
+  return pow(10.0, log_val);
+}
+
+template <int V>
+MHPPO_HD inline bool choix_pedestrian(Env<V> &E, const Ped &q, int mode) {
+  const double car_size = 4;
+  int n = 0;
+  for (int s = 0; s < E.c.nC; s++) n += in_view(E, s, mode);
+  if (q.has(F_FOLLOW)) {
+    if (V == V_NAIF) {
+      // random.shuffle(cars): real permutation, nibble-packed (n <= 16)
+      uint64_t perm = 0;
+      for (int i = 0; i < n; i++) perm |= (uint64_t)i << (4 * i);
+      if (n > 1) {
+        for (int i = n - 1; i >= 1; i--) {
+          int j = (int)E.rng.randbelow((uint32_t)(i + 1));
+          uint64_t xi = (perm >> (4 * i)) & 15u, xj = (perm >> (4 * j)) & 15u;
+          perm &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+          perm |= (xj << (4 * i)) | (xi << (4 * j));
+        }
+      }
+      // naif: view == all slots, in order
+      for (int k = 0; k < n; k++) {
+        int i = (int)((perm >> (4 * k)) & 15u);
+        double pos = E.car(C_SC, i), line = E.car(C_LINE, i);
+        if (is_crossing_in_front(E, q, line, 0.5) && is_in_front(E, q, line, 1.0) &&
+            (pos < car_size + q.Sx) && (pos > q.Sx))
+          return false;
+      }
+      for (int k = 0; k < n; k++) {
+        int i = (int)((perm >> (4 * k)) & 15u);
+        if (E.car(C_SC, i) < q.Sx && E.car(C_LIGHT, i) < 0) return false;
+      }
+    } else {
+      if (V != V_4CARS && n > 1)
+        for (int i = n - 1; i >= 1; i--) (void)E.rng.randbelow((uint32_t)(i + 1));
+      for (int s = 0; s < E.c.nC; s++) {
+        if (!in_view(E, s, mode)) continue;
+        double pos = E.car(C_SC, s), line = E.car(C_LINE, s);
+        if (is_crossing_in_front(E, q, line, 0.5) && is_in_front(E, q, line, 1.0)) {
+          if ((pos < car_size + q.Sx) && (pos > q.Sx)) return false;
+        }
+      }
+      for (int s = 0; s < E.c.nC; s++) {
+        if (!in_view(E, s, mode)) continue;
+        double light = E.car(C_LIGHT, s);
+        if (E.car(C_SC, s) < q.Sx && light != 0) return light > 0.;
+      }
+    }
+  }
+  for (int s = 0; s < E.c.nC; s++) {
+    if (!in_view(E, s, mode)) continue;
+    double line = E.car(C_LINE, s);
+    if (is_in_front(E, q, line, 1.0)) {
+      double pos = E.car(C_SC, s);
+      if ((pos < car_size + q.Sx) && (pos > q.Sx)) return false;
+      if (pos < q.Sx) {
+        double car_time = fabs((pos - q.Sx) / (E.car(C_VC, s) + 10e-3));
+        double CG = CG_score(E, q, fabs(q.lpos - line) * E.cross);
+        if (car_time + E.car(C_LIGHT, s) < CG) return false;
+      }
+    }
+  }
+  return true;
+}
+
+template <int V>
+MHPPO_HD inline double worst_delta_l(const Env<V> &E, const Ped &q, double pos, double spd, double line) {
+  if (pos > q.Sx || q.has(F_LEFT) || !is_in_front(E, q, line, 0)) return V == V_SCALABLE ? 100.0 : 0.0;
+  return fabs(pos - q.Sx) - (spd * spd / (-2.0 * E.c.b00));
+}
+
+template <int V>
+MHPPO_HD inline double delta_l(const Env<V> &E, const Ped &q, double pos, double spd, double line) {
+  if (pos > q.Sx || q.has(F_LEFT) || !is_in_front(E, q, line, 0)) return 0.0;
+  return fabs(pos - q.Sx) - (spd * spd / (-2.0 * E.c.b00)) - 1.0 * (spd);
+}
+
+template <int V>
+MHPPO_HD inline double delta_l_all(const Env<V> &E, const Ped &q, int mode) {
+  double dl = V == V_SCALABLE ? 100.0 : 0.0;
+  for (int s = 0; s < E.c.nC; s++) {
+    if (!in_view(E, s, mode)) continue;
+    double pos = E.car(C_SC, s), spd = E.car(C_VC, s);
+    if ((pos <= q.Sx) && is_in_front(E, q, E.car(C_LINE, s), 0) && (!q.has(F_LEFT)) && (E.car(C_LIGHT, s) >= 0)) {
+      double nd = fabs(pos - q.Sx) - (spd * spd / (-2.0 * E.c.b00)) - 1.0 * (spd);
+      dl = pymin(dl, nd);
+    }
+  }
+  return dl;
+}
+
+// pedestrian.get_data (:433-444); updates the running-min `delta`
+template <int V>
+MHPPO_HD inline void ped_get_data(const Env<V> &E, Ped &q, int mode, double out[9]) {
+  if (!q.has(F_EXIST)) {
+    for (int k = 0; k < 9; k++) out[k] = 0.;
+    return;
+  }
+  q.delta = pymin(delta_l_all(E, q, mode) * (double)q.has(F_ISCROSS) * (double)(!q.has(F_LEFT)), q.delta);
+  out[0] = q.Vx; out[1] = q.Vy; out[2] = q.Sx; out[3] = q.Sy; out[4] = q.delta;
+  out[5] = q.has(F_LEFT); out[6] = q.has(F_INCROSS); out[7] = 1.0; out[8] = (double)q.dir;
+}
+
+template <int V>
+MHPPO_HD inline double new_reward_wait_safety(const Env<V> &E, Ped &q, double spd, double pos, double line) {
+  if ((!q.has(F_LEFT)) && q.has(F_ISCROSS) && (pos < q.Sx) && is_in_front(E, q, line, 0)) {
+    double exp_dl;
+    if (spd < 0.05) {
+      exp_dl = 0.;
+    } else {
+      double dl = delta_l(E, q, pos, spd, line) / (spd);
+      if (dl >= -1.) exp_dl = pymax(-20. * exp(-4. * (dl)-4.), -20.0);
+      else exp_dl = 20. * dl;
+    }
+    exp_dl = exp_dl - (double)(q.has(F_ACCIDENT) ? 20 : 0);
+    if (exp_dl < q.wdl) q.wdl = exp_dl;
+  }
+  return q.wdl + 0.0;
+}
+
+// --------------------------------------------------------- pedestrian.step
+template <int V>
+MHPPO_HD inline void function_step(const Env<V> &E, const Ped &q, double time, double &pos, double &spd) {
+  if (q.has(F_SIN)) {
+    double t = time + E.c.dt;
+    double speed_p = (q.A * sin(q.W * (t - q.t0)) + q.B);
+    double pos_p = ((-E.cl / 2.) + (q.A * (-cos(q.W * (t - q.t0)) + cos(q.W * 0.0)) / q.W));
+    if (!(pos_p >= 0.0 && speed_p < fabs(q.ivy))) {
+      pos = (double)q.dir * pos_p;
+      spd = (double)q.dir * speed_p;
+      return;
+    }
+  }
+  pos = q.Sy + q.ivy * E.c.dt;
+  spd = q.ivy;
+}
+
+template <int V>
+MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
+  const double dt = E.c.dt, cl = E.cl;
+  double pp_y = q.Sy + q.ivy * dt;
+  {  // boolean_ped_position (:261-274)
+    double ds = (double)q.dir * q.Sy;
+    if (ds >= cl / 2) { q.set(F_INCROSS, false); q.set(F_LEFT, true); }
+    else if (ds > -cl / 2) { q.set(F_INCROSS, true); q.set(F_LEFT, false); }
+    else { q.set(F_INCROSS, false); q.set(F_LEFT, false); }
+  }
+  if (!q.has(F_ISCROSS)) return;
+  bool choose = true;
+  if (!q.has(F_DECISION) && q.has(F_ATCROSS)) {
+    choose = choix_pedestrian(E, q, 1);
+    if (choose) {
+      q.lpos = (double)((E.c.nb_lines - 1) * (q.dir < 0));
+      q.set(F_ATCROSS, false);
+    }
+    q.set(F_DECISION, true);
+    q.t0 = time;
+  }
+  const double dir = (double)q.dir;
+  if ((q.Sy * dir < -cl / 2.) && (pp_y * dir > -cl / 2.) && !q.has(F_DECISION)) {
+    double pos_p_x = (q.Vx * dt) * (fabs(-cl / 2. - q.Sy * dir) / fabs(q.Vy * dt + 10e-3));
+    q.Vx = pos_p_x / dt;
+    q.Sx = q.Sx + pos_p_x;
+    q.Vy = dir * fabs(-q.Sy * dir - (cl / 2.)) / dt;
+    q.Sy = -dir * cl / 2.;
+    q.tstop = 0;
+    q.set(F_ATCROSS, true);
+  } else if ((fabs(q.Sy) <= cl / 2) || q.has(F_DECISION)) {
+    if (q.tstop != 0) {
+      q.Vx = 0.0;
+      q.Vy = 0.0;
+      q.tstop = q.tstop - 1;
+      q.t0 = q.t0 + dt;
+    } else if ((E.rng.uniform(0, 1) < 0.98) && choose) {
+      q.set(F_DECISION, false);
+      double new_spy, new_vpy;
+      function_step(E, q, time, new_spy, new_vpy);
+      bool change_line = false;
+      if (fabs(new_spy) < cl / 2) {  // will_change_line (:276-281)
+        double new_line = py_floordiv(new_spy + cl / 2, E.cross);
+        if (new_line != q.lpos && fabs(q.Sy) < cl / 2) change_line = true;
+      }
+      double dtc = ((double)E.c.nb_lines - q.lpos - 1) * E.cross * (double)(q.dir > 0);
+      dtc += (q.lpos) * E.cross * (double)(q.dir < 0);
+      bool new_choice;
+      if (change_line && (dtc > 0. && dtc < cl)) {
+        new_choice = choix_pedestrian(E, q, 1);
+        if (new_choice && q.has(F_STOP)) q.set(F_STOP, false);
+      } else {
+        new_choice = false;
+      }
+      if (q.has(F_STOP)) {
+        q.Vx = 0.0;
+        q.Vy = 0.0;
+        q.t0 = q.t0 + dt;
+        if (change_line) q.wt = q.wt + dt;
+      } else if (V == V_SCALABLE && q.has(F_NEEDSTOP) && q.Sy < q.cstop && pp_y > q.cstop) {
+        q.tstop = E.rng.randint(5, 35);
+        q.set(F_NEEDSTOP, false);
+        if (!choose) {
+          q.set(F_DECISION, false);
+          q.tstop = 0;
+          q.wt = q.wt + dt;
+        }
+        q.Vx = 0.0;
+        q.Vy = 0.0;
+        q.t0 = q.t0 + dt;
+      } else if ((!change_line) || (change_line && new_choice)) {
+        q.Sy = new_spy;
+        q.Vy = new_vpy;
+        double nsx = q.Sx + q.Vy * q.ratio * dt, nvx = q.Vy * q.ratio;
+        q.Sx = nsx;
+        q.Vx = nvx;
+        q.ct = q.ct + dt;
+        if (change_line && new_choice) {  // apply_change_line (:283-289)
+          if (fabs(new_spy) >= cl / 2) {
+            q.lpos = (double)(E.c.nb_lines * (q.dir < 0) - 1 * (q.dir > 0));
+          } else {
+            double new_line = py_floordiv(new_spy + cl / 2, E.cross);
+            if (new_line != q.lpos) q.lpos = new_line;
+          }
+        }
+      } else {  // change_line && !new_choice
+        q.set(F_STOP, true);
+        double distance = fabs(dir * (cl - dtc) - dir * cl / 2. - q.Sy);
+        double pos_p_x = (q.Vx) * (distance) / fabs(q.Vy + 10e-3);
+        q.Vx = pos_p_x / dt;
+        q.Sx = q.Sx + pos_p_x;
+        q.Vy = dir * distance / dt;
+        q.Sy = dir * ((cl - dtc) - cl / 2.);
+      }
+    } else {
+      q.tstop = E.rng.randint(2, 5);
+      if (!choose) {
+        q.set(F_DECISION, false);
+        q.tstop = 0;
+        q.wt = q.wt + dt;
+      }
+      q.Vx = 0.0;
+      q.Vy = 0.0;
+      q.t0 = q.t0 + dt;
+    }
+  } else {
+    double nsx = q.Sx + q.ivx * dt, nsy = q.Sy + q.ivy * dt;
+    q.Sx = nsx;
+    q.Vx = q.ivx;
+    q.Sy = nsy;
+    q.Vy = q.ivy;
+  }
+}
+
+// ------------------------------------------------------- pedestrian.detection
+// accumulates this ped's per-slot danger into acc[] (caller passes registers)
+template <int V, int MAXS>
+MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double *acc, bool add) {
+  const int nS = E.c.nS;
+  for (int i = 0; i < nS; i++) {
+    bool cond = is_in_front(E, q, E.car(C_LINE, i), 0);
+    if (V == V_SCALABLE) cond = cond && (E.car(C_EXIST, i) != 0.0);
+    if (!cond) continue;
+    double Sc = E.car(C_SC, i), Vc = E.car(C_VC, i), line = E.car(C_LINE, i);
+    int ped_accident;
+    if (V == V_NAIF) {
+      q.set(F_WSA, worst_delta_l(E, q, Sc, Vc, line) < 0);
+      ped_accident = (!q.has(F_ACCIDENT)) && q.has(F_WSA);
+    } else {
+      ped_accident = (!q.has(F_ACCIDENT)) && q.has(F_WSA);
+      q.set(F_WSA, worst_delta_l(E, q, Sc, Vc, line) < 0);
+    }
+    bool cif = is_crossing_in_front(E, q, line, 0);
+    if (ped_accident && (cif && (prev[i] < q.Sx) && (Sc > q.Sx))) q.set(F_ACCIDENT, true);
+    if (cif) {
+      double dl;
+      if ((Vc) < 0.05) dl = (V == V_SCALABLE) ? 100. : 0.;
+      else dl = worst_delta_l(E, q, Sc, Vc, line) / (Vc);
+      double pa;
+      if (dl > 0) pa = -1. * exp(-4. * (dl));
+      else pa = (V == V_NAIF) ? -1. * dl - 1 : 1. * dl - 1;
+      E.car(C_PA, i) = pymin(E.car(C_PA, i), pa);
+    }
+    double Ts = E.car(C_TS, i);
+    double tb = -(10.0 / (2.0 * E.c.b00)) + 1.;  // car.time_braking (:564), Vc = speed_limit at init
+    if (V == V_NAIF) {
+      if (Sc < q.Sx) Ts = pymax(q.wt + 10. * q.ct - tb + 1., Ts);
+    } else {
+      double clw = 0;
+      for (int k = 0; k < nS; k++)
+        if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0))
+          clw += 1.0;
+      if (Sc < q.Sx) Ts = pymax((1. + clw) * q.wt + 2. * q.ct - tb + 1., Ts);
+    }
+    E.car(C_TS, i) = Ts;
+    double light = E.car(C_LIGHT, i);
+    if (light < 0.0) {
+      double ne = (Ts < 0) ? -1. * exp(4. * (Ts)) : -1. * (1 + Ts);
+      E.car(C_ES, i) = pymin(ne, E.car(C_ES, i));
+    }
+    if (light > 0.0) {
+      double ne = (q.Sx - Sc > 0) ? -1. * exp(-4. * (q.Sx - Sc)) : -1. * (1 + Sc - q.Sx);
+      E.car(C_ES, i) = pymin(ne, E.car(C_ES, i));
+    }
+  }
+  if (!add) return;
+  double green = 0;
+  for (int k = 0; k < nS; k++)
+    if (E.car(C_LIGHT, k) > 0. && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0)) green += 1.0;
+  for (int i = 0; i < nS && i < MAXS; i++) {
+    double res = E.car(C_PA, i) + E.car(C_ES, i);
+    double term = 0.5 * green * (double)(E.car(C_LIGHT, i) < 0.) * (double)(E.car(C_TS, i) > 0);
+    if (V == V_COOP) res = res + term;
+    else if (V == V_4CARS || V == V_SCALABLE) res = res - term;
+    if (V == V_SCALABLE && E.car(C_EXIST, i) == 0.0) res = 0.;
+    acc[i] += res;
+  }
+}
+
+// ---------------------------------------------------------------- car.step
+template <int V>
+MHPPO_HD inline double car_follow_action(const Env<V> &E, int s, double lead_V, double lead_S) {
+  double speed_car = E.car(C_VC, s);
+  double diff_dist = lead_S - E.car(C_SC, s);
+  double delta_v = speed_car - lead_V;
+  double sm = 2. + (speed_car * 2.0) + (speed_car * delta_v) / E.c.idm_den;
+  return E.c.b10 * (1 - pow(speed_car / 10., 4.0) - pow(sm / diff_dist, 2.0));
+}
+
+template <int V>
+MHPPO_HD inline void car_step(const Env<V> &E, int s, double action, double light) {
+  const double dt = E.c.dt;
+  double Vc = E.car(C_VC, s);
+  double acc = pymin(pymax(action, E.c.b00), E.c.b10);
+  double sg;
+  if (Vc == 0.) sg = pymax(0., acc / fabs(acc));
+  else if (acc > 0) sg = 1;
+  else sg = pymax(pymin(-Vc / (dt * acc), 1.), 0.);
+  double h0 = E.car(C_H0, s), h1 = E.car(C_H1, s);
+  double fa = 0.0;
+  fa = fa + 1.0 * acc;
+  fa = fa + 0. * h0;
+  fa = fa + 0. * h1;
+  E.car(C_H1, s) = h0;
+  E.car(C_H0, s) = acc;
+  fa = fa * sg;
+  double speed = Vc + dt * fa;
+  double pos = (fa * E.c.dt2 / 2.0) + (Vc * dt) + (E.car(C_SC, s));
+  E.car(C_AC, s) = fa;
+  E.car(C_VC, s) = speed;
+  E.car(C_SC, s) = pos;
+  E.car(C_LIGHT, s) = light;
+}
+
+MHPPO_HD inline double car_reward(double Vc) { return -10. * pow(Vc - 10.0, 2.0) / 100.0; }
+
+}  // namespace mhppo

@@ -1,0 +1,169 @@
+// mhppo_env.hip — crosswalk env kernels (create/reset/step/state) + their C-ABI.
+//
+// One env per lane, 256-thread workgroups (4 waves), grid = ceil(N/256).
+// The launch is variant-templated so each reference env class compiles to
+// its own straight-line kernel with no variant branches.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/mhppo.h"
+#include "common.h"
+#include "env_body.h"
+
+using namespace mhppo;
+
+namespace {
+constexpr int TPB = 256;
+
+// ------------------------------------------------------------- kernels
+template <int V>
+__global__ void __launch_bounds__(TPB) k_env_reset(Cfg c, Bufs b, float *obs) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  if (e < c.N) env_reset_one<V>(c, b, e, obs);
+}
+
+template <int V>
+__global__ void __launch_bounds__(TPB)
+    k_env_step(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  if (e < c.N) env_step_one<V>(c, b, e, actions, obs, rew, rlight, done);
+}
+
+__global__ void __launch_bounds__(TPB) k_env_seed(Cfg c, Bufs b) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  if (e < c.N) env_seed_one(c, b, e);
+}
+
+template <int V>
+__global__ void __launch_bounds__(TPB) k_env_state(Cfg c, Bufs b, double *out, int dim) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  if (e < c.N) env_state_one<V>(c, b, e, out, dim);
+}
+
+__global__ void k_env_rng(Cfg c, Bufs b, uint32_t *mt, int32_t *mti) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < (size_t)c.N * 624) mt[i] = b.mt[i];
+  if (i < (size_t)c.N) mti[i] = b.envi[EI_MTI * c.N + i];
+}
+
+}  // namespace
+
+struct mhppo_env {
+  Cfg c;
+  Bufs b;
+  int device;
+  void *blob;
+};
+
+#define VARIANT_LAUNCH(kern, variant, grid, stream, ...)                                    \
+  do {                                                                                      \
+    switch (variant) {                                                                      \
+      case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;   \
+      case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break; \
+      case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break; \
+      default: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;       \
+    }                                                                                       \
+  } while (0)
+
+extern "C" {
+
+int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
+  if (!cfg || !out) return set_error(MHPPO_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->variant < 0 || cfg->variant > 3) return set_error(MHPPO_EINVAL, "unknown variant %d", cfg->variant);
+  if (cfg->n_envs <= 0) return set_error(MHPPO_EINVAL, "n_envs must be > 0");
+  if (cfg->nb_car < 1 || cfg->nb_ped < 1 || cfg->nb_lines < 1 || cfg->nb_ped > 8)
+    return set_error(MHPPO_EINVAL, "bad nb_car/nb_ped/nb_lines");
+  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : cfg->nb_car;
+  if (nS > MAXS) return set_error(MHPPO_EINVAL, "too many car slots (%d > %d)", nS, MAXS);
+  if (cfg->variant == V_SCALABLE && cfg->nb_car > nS)
+    return set_error(MHPPO_EINVAL, "scalable: nb_car must be <= 2*nb_lines (random.sample)");
+  if (cfg->variant == V_NAIF && nS > 16) return set_error(MHPPO_EINVAL, "naif: at most 16 cars");
+  if (!(cfg->car_b[0] < 0.0)) return set_error(MHPPO_EINVAL, "car_b[0][0] must be negative");
+  CHECK_HIP(hipSetDevice(device));
+  mhppo_env *h = new mhppo_env();
+  build_cfg(*cfg, h->c);
+  const Cfg &c = h->c;
+  h->device = device;
+  size_t N = (size_t)c.N;
+  size_t bytes_car = sizeof(double) * C_NF * c.nC * N, bytes_ped = sizeof(double) * P_NF * c.P * N;
+  size_t bytes_pfl = sizeof(uint32_t) * c.P * N, bytes_envd = sizeof(double) * E_ND * N;
+  size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * 624 * N;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_mt);
+  if (hipMalloc(&h->blob, total) != hipSuccess) {
+    delete h;
+    return set_error(MHPPO_ENOMEM, "hipMalloc(%zu) failed", total);
+  }
+  char *p = (char *)h->blob;
+  h->b.car = (double *)p; p += al(bytes_car);
+  h->b.ped = (double *)p; p += al(bytes_ped);
+  h->b.pfl = (uint32_t *)p; p += al(bytes_pfl);
+  h->b.envd = (double *)p; p += al(bytes_envd);
+  h->b.envi = (int32_t *)p; p += al(bytes_envi);
+  h->b.mt = (uint32_t *)p;
+  hipMemset(h->blob, 0, total);
+  dim3 grid((c.N + TPB - 1) / TPB);
+  hipLaunchKernelGGL(k_env_seed, grid, dim3(TPB), 0, (hipStream_t)0, c, h->b);
+  CHECK_HIP(hipGetLastError());
+  CHECK_HIP(hipDeviceSynchronize());
+  *out = h;
+  return MHPPO_OK;
+}
+
+void mhppo_env_destroy(mhppo_env *env) {
+  if (!env) return;
+  hipSetDevice(env->device);
+  hipFree(env->blob);
+  delete env;
+}
+
+int mhppo_env_obs_dim(const mhppo_env *env) { return env ? env->c.obs_dim : MHPPO_EINVAL; }
+int mhppo_env_slots(const mhppo_env *env) { return env ? env->c.nS : MHPPO_EINVAL; }
+int mhppo_env_state_dim(const mhppo_env *env) { return env ? 20 * env->c.P + 8 * env->c.nC + 4 : MHPPO_EINVAL; }
+
+int mhppo_env_reset(mhppo_env *env, float *obs, void *stream) {
+  if (!env) return set_error(MHPPO_EINVAL, "null env");
+  dim3 grid((env->c.N + TPB - 1) / TPB);
+  VARIANT_LAUNCH(k_env_reset, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, obs);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *rewards, double *reward_light,
+                   uint8_t *done, void *stream) {
+  if (!env || !actions) return set_error(MHPPO_EINVAL, "null env/actions");
+  dim3 grid((env->c.N + TPB - 1) / TPB);
+  VARIANT_LAUNCH(k_env_step, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, actions, obs, rewards,
+                 reward_light, done);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_env_get_state(mhppo_env *env, double *out, void *stream) {
+  if (!env || !out) return set_error(MHPPO_EINVAL, "null env/out");
+  dim3 grid((env->c.N + TPB - 1) / TPB);
+  int dim = mhppo_env_state_dim(env);
+  VARIANT_LAUNCH(k_env_state, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, out, dim);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_env_get_rng(mhppo_env *env, uint32_t *mt, int32_t *mti, void *stream) {
+  if (!env || !mt || !mti) return set_error(MHPPO_EINVAL, "null argument");
+  size_t n = (size_t)env->c.N * 624;
+  dim3 grid((unsigned)((n + TPB - 1) / TPB));
+  hipLaunchKernelGGL(k_env_rng, grid, dim3(TPB), 0, (hipStream_t)stream, env->c, env->b, mt, mti);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+}  // extern "C"
+
+// internal accessors for the rollout kernels (same library)
+namespace mhppo {
+const Cfg &env_cfg(const mhppo_env *env) { return env->c; }
+const Bufs &env_bufs(const mhppo_env *env) { return env->b; }
+}  // namespace mhppo

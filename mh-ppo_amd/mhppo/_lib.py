@@ -1,0 +1,90 @@
+"""ctypes binding of libmhppo.so (include/mhppo.h).
+
+The HIP library is the product path: there is no CPU or PyTorch fallback.  If
+the shared object is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmhppo.so")
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F64 = ctypes.c_double
+
+
+class EnvCfg(ctypes.Structure):
+    _fields_ = [
+        ("variant", I32), ("n_envs", I32), ("nb_car", I32), ("nb_ped", I32), ("nb_lines", I32),
+        ("max_episode", I32), ("sin_model", I32), ("reserved", I32), ("dt", F64),
+        ("car_b", F64 * 4), ("ped_b", F64 * 8), ("cross_b", F64 * 2), ("seed_base", U64),
+        ("env_id_offset", U64),
+    ]
+
+
+class Mlp(ctypes.Structure):
+    _fields_ = [("w1", P), ("b1", P), ("w2", P), ("b2", P), ("w3", P), ("b3", P), ("w4", P), ("b4", P),
+                ("n_in", I32), ("n_out", I32)]
+
+
+# name: (restype, argtypes)
+_SIGS = {
+    "mhppo_env_create": (I32, [ctypes.POINTER(EnvCfg), I32, ctypes.POINTER(P)]),
+    "mhppo_env_destroy": (None, [P]),
+    "mhppo_env_obs_dim": (I32, [P]),
+    "mhppo_env_slots": (I32, [P]),
+    "mhppo_env_state_dim": (I32, [P]),
+    "mhppo_env_reset": (I32, [P, P, P]),
+    "mhppo_env_step": (I32, [P, P, P, P, P, P, P]),
+    "mhppo_env_get_state": (I32, [P, P, P]),
+    "mhppo_env_get_rng": (I32, [P, P, P, P]),
+    "mhppo_last_error": (ctypes.c_char_p, []),
+    "mhppo_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class MhppoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmhppo.so once; raise loudly if it is absent (no fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MhppoError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def check(rc):
+    if rc != 0:
+        raise MhppoError(f"libmhppo error {rc}: {lib().mhppo_last_error().decode()}")
+    return rc
+
+
+def ptr(t):
+    """Device (or host) pointer of a torch tensor / None."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

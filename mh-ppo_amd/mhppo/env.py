@@ -1,0 +1,117 @@
+"""Vectorised crosswalk envs on the GPU: N reference envs per handle.
+
+`VecCrosswalk` owns one libmhppo env handle (device state + N CPython-compatible
+random streams) and exchanges torch tensors on the handle's device.  It is the
+batched form of the reference Gym env
+(`Crosswalk_hybrid_multi_*.reset/step`, Environments/Env_hybrid_multi_coop.py
+:745-893); `mhppo.envs` wraps it back into the single-env Gym surface.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3}
+CAR_B = ((-4.0, 10.0), (2.0, 10.0))   # Coop-MH-PPO-scalable.py:1007
+PED_B = ((-0.05, 0.75, 0.0, -3.0), (0.05, 1.75, 4.0, -0.5))  # :1008
+CROSS_B = (2.5, 3.0)  # :1009
+
+
+def _flat(x, n):
+    import numpy as np
+    a = np.asarray(x, dtype=np.float64).reshape(-1)
+    if a.size != n:
+        raise ValueError(f"expected {n} values, got {a.size}")
+    return a
+
+
+class VecCrosswalk:
+    """N independent crosswalk envs of one reference variant on one GPU.
+
+    Env `e` draws from `random.seed(seed_base + env_id_offset + e)`, so a shard
+    of envs on rank r reproduces exactly the trajectories the same global env
+    ids have on a single GPU.
+    """
+
+    def __init__(self, variant, n_envs, nb_car, nb_ped, nb_lines, dt=0.3, max_episode=80,
+                 simulation="sin", car_b=CAR_B, ped_b=PED_B, cross_b=CROSS_B, seed_base=0,
+                 env_id_offset=0, device=None):
+        self.variant = variant
+        self.device = torch.device(device if device is not None else "cuda")
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", dev_index)
+        cfg = _lib.EnvCfg()
+        cfg.variant = VARIANTS[variant]
+        cfg.n_envs = n_envs
+        cfg.nb_car, cfg.nb_ped, cfg.nb_lines = nb_car, nb_ped, nb_lines
+        cfg.max_episode = max_episode
+        cfg.sin_model = int(simulation == "sin")
+        cfg.dt = dt
+        for i, v in enumerate(_flat(car_b, 4)):
+            cfg.car_b[i] = v
+        for i, v in enumerate(_flat(ped_b, 8)):
+            cfg.ped_b[i] = v
+        for i, v in enumerate(_flat(cross_b, 2)):
+            cfg.cross_b[i] = v
+        cfg.seed_base = seed_base
+        cfg.env_id_offset = env_id_offset
+        self.cfg = cfg
+        self.n_envs, self.nb_car, self.nb_ped, self.nb_lines = n_envs, nb_car, nb_ped, nb_lines
+        self.dt, self.max_episode = dt, max_episode
+        h = ctypes.c_void_p()
+        L = _lib.lib()
+        with torch.cuda.device(self.device):
+            _lib.check(L.mhppo_env_create(ctypes.byref(cfg), dev_index, ctypes.byref(h)))
+        self._h = h
+        self.obs_dim = L.mhppo_env_obs_dim(h)
+        self.n_slots = L.mhppo_env_slots(h)
+        self.state_dim = L.mhppo_env_state_dim(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().mhppo_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _t(self, shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    def reset(self, want_obs=True):
+        obs = self._t((self.n_envs, self.obs_dim), torch.float32) if want_obs else None
+        _lib.check(_lib.lib().mhppo_env_reset(self._h, _lib.ptr(obs), _lib.stream_ptr()))
+        return obs
+
+    def step(self, actions, want_obs=True):
+        """actions: float64 [N, 2S] (acc..., light...) on the device."""
+        a = actions.to(device=self.device, dtype=torch.float64).contiguous()
+        if a.shape != (self.n_envs, 2 * self.n_slots):
+            raise ValueError(f"actions must be [{self.n_envs}, {2 * self.n_slots}], got {tuple(a.shape)}")
+        obs = self._t((self.n_envs, self.obs_dim), torch.float32) if want_obs else None
+        rew = self._t((self.n_envs, self.n_slots), torch.float64)
+        rl = self._t((self.n_envs, self.n_slots), torch.float64)
+        done = self._t((self.n_envs,), torch.uint8)
+        _lib.check(_lib.lib().mhppo_env_step(self._h, _lib.ptr(a), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(rl),
+                                             _lib.ptr(done), _lib.stream_ptr()))
+        return obs, rew, rl, done.bool()
+
+    def get_state(self):
+        """[N, state_dim] float64: per ped 20, per car slot 8, then cross, time, ped_traffic, car_traffic."""
+        out = self._t((self.n_envs, self.state_dim), torch.float64)
+        _lib.check(_lib.lib().mhppo_env_get_state(self._h, _lib.ptr(out), _lib.stream_ptr()))
+        return out
+
+    def get_rng(self):
+        mt = self._t((self.n_envs, 624), torch.int32)
+        mti = self._t((self.n_envs,), torch.int32)
+        _lib.check(_lib.lib().mhppo_env_get_rng(self._h, _lib.ptr(mt), _lib.ptr(mti), _lib.stream_ptr()))
+        return mt, mti

@@ -104,3 +104,13 @@ class OracleEnv:
         mti = np.zeros(1, np.int32)
         lib().oracle_env_get_rng(self.h, _p(mt), _p(mti))
         return mt, int(mti[0])
+
+
+def rng_stream(seed, kind, n, a=0.0, b=0.0, per=1):
+    L = lib()
+    L.oracle_rng_stream.restype = ctypes.c_int
+    L.oracle_rng_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_int, ctypes.c_void_p]
+    out = np.zeros(n * per, np.float64)
+    k = L.oracle_rng_stream(seed, kind, a, b, n, _p(out))
+    return out[:k]

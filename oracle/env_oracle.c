@@ -788,3 +788,35 @@ int oracle_env_dump(const OEnv *e, double *out) {
     }
     return k;
 }
+
+/* ---- CPython random restatement, exported for its own pin test ---------- */
+/* kind: 0 random(), 1 randint(a,b), 2 uniform(a,b), 3 normalvariate(a,b),
+ *       4 randbelow(a), 5 shuffle(range(a)) flattened, 6 sample(range(a), b) flattened */
+int oracle_rng_stream(uint64_t seed, int kind, double a, double b, int n, double *out) {
+    PyRandom r;
+    pyr_seed(&r, seed);
+    int k = 0;
+    for (int i = 0; i < n; i++) {
+        switch (kind) {
+        case 0: out[k++] = pyr_random(&r); break;
+        case 1: out[k++] = (double)pyr_randint(&r, (long)a, (long)b); break;
+        case 2: out[k++] = pyr_uniform(&r, a, b); break;
+        case 3: out[k++] = pyr_normalvariate(&r, a, b); break;
+        case 4: out[k++] = (double)pyr_randbelow(&r, (uint32_t)a); break;
+        case 5: {
+            int x[64], m = (int)a;
+            for (int j = 0; j < m; j++) x[j] = j;
+            pyr_shuffle(&r, x, m);
+            for (int j = 0; j < m; j++) out[k++] = x[j];
+            break;
+        }
+        case 6: {
+            int x[64];
+            pyr_sample_range(&r, (int)a, (int)b, x);
+            for (int j = 0; j < (int)b; j++) out[k++] = x[j];
+            break;
+        }
+        }
+    }
+    return k;
+}

@@ -1,0 +1,43 @@
+"""The device env source (mh-ppo_amd/csrc/env_body.h), compiled for the CPU by
+tools/hostsim.cpp, reproduces the reference fixtures bit-exactly.
+
+With host libm (glibc, what CPython uses) there is no transcendental ULP gap,
+so this pins the kernel's LOGIC: RNG draw order, branch structure, Python
+min/max/floordiv semantics.  The GPU test (test_env_gpu.py) then only has to
+account for device-libm ULPs.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FILES = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "env_*.npz")))
+
+
+@pytest.fixture(scope="module")
+def hostsim():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tools")])
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import hostsim as hs
+    return hs
+
+
+@pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f)[4:-4] for f in FILES])
+def test_device_source_matches_reference(hostsim, path):
+    g = np.load(path)
+    E, T = g["obs"].shape[:2]
+    h = hostsim.HostVec(str(g["variant"]), E, int(g["nb_car"]), int(g["nb_ped"]), int(g["nb_lines"]),
+                        seed_base=int(g["seed_base"]))
+    assert np.array_equal(h.reset(), g["obs0"])
+    k = g["dump"].shape[2]
+    for t in range(T):
+        o, r, rl, d = h.step(g["actions"][:, t])
+        assert np.array_equal(o, g["obs"][:, t]), t
+        assert np.array_equal(r, g["rewards"][:, t]), t
+        assert np.array_equal(rl, g["reward_light"][:, t]), t
+        assert np.array_equal(d, g["done"][:, t]), t
+        assert np.array_equal(h.state()[:, :k], g["dump"][:, t]), t

@@ -1,0 +1,66 @@
+// hostsim.cpp — runs the device env source (env_body.h) on the CPU, one env at a
+// time, for debugging the HIP path against the oracle without a GPU.  Host libm
+// (glibc) is used for transcendentals, so any mismatch vs the oracle is logic.
+// Build: make -C tools hostsim   ->  tools/libhostsim.so (ctypes)
+#include <stdlib.h>
+#include <string.h>
+
+#include "../mh-ppo_amd/csrc/env_body.h"
+
+using namespace mhppo;
+
+struct HostEnv {
+  Cfg c;
+  Bufs b;
+  void *blob;
+};
+
+extern "C" {
+HostEnv *hs_create(const mhppo_env_cfg *cfg) {
+  HostEnv *h = new HostEnv();
+  build_cfg(*cfg, h->c);
+  const Cfg &c = h->c;
+  size_t N = c.N;
+  h->b.car = (double *)calloc((size_t)C_NF * c.nC * N, 8);
+  h->b.ped = (double *)calloc((size_t)P_NF * c.P * N, 8);
+  h->b.pfl = (uint32_t *)calloc((size_t)c.P * N, 4);
+  h->b.envd = (double *)calloc((size_t)E_ND * N, 8);
+  h->b.envi = (int32_t *)calloc((size_t)EI_NI * N, 4);
+  h->b.mt = (uint32_t *)calloc((size_t)624 * N, 4);
+  for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
+  return h;
+}
+int hs_obs_dim(HostEnv *h) { return h->c.obs_dim; }
+int hs_state_dim(HostEnv *h) { return 20 * h->c.P + 8 * h->c.nC + 4; }
+void hs_reset(HostEnv *h, float *obs) {
+  for (int e = 0; e < h->c.N; e++) {
+    switch (h->c.variant) {
+      case V_COOP: env_reset_one<V_COOP>(h->c, h->b, e, obs); break;
+      case V_4CARS: env_reset_one<V_4CARS>(h->c, h->b, e, obs); break;
+      case V_SCALABLE: env_reset_one<V_SCALABLE>(h->c, h->b, e, obs); break;
+      default: env_reset_one<V_NAIF>(h->c, h->b, e, obs);
+    }
+  }
+}
+void hs_step(HostEnv *h, const double *a, float *obs, double *rew, double *rl, uint8_t *done) {
+  for (int e = 0; e < h->c.N; e++) {
+    switch (h->c.variant) {
+      case V_COOP: env_step_one<V_COOP>(h->c, h->b, e, a, obs, rew, rl, done); break;
+      case V_4CARS: env_step_one<V_4CARS>(h->c, h->b, e, a, obs, rew, rl, done); break;
+      case V_SCALABLE: env_step_one<V_SCALABLE>(h->c, h->b, e, a, obs, rew, rl, done); break;
+      default: env_step_one<V_NAIF>(h->c, h->b, e, a, obs, rew, rl, done);
+    }
+  }
+}
+void hs_state(HostEnv *h, double *out) {
+  int dim = hs_state_dim(h);
+  for (int e = 0; e < h->c.N; e++) {
+    switch (h->c.variant) {
+      case V_COOP: env_state_one<V_COOP>(h->c, h->b, e, out, dim); break;
+      case V_4CARS: env_state_one<V_4CARS>(h->c, h->b, e, out, dim); break;
+      case V_SCALABLE: env_state_one<V_SCALABLE>(h->c, h->b, e, out, dim); break;
+      default: env_state_one<V_NAIF>(h->c, h->b, e, out, dim);
+    }
+  }
+}
+}
