@@ -80,69 +80,88 @@ int mhppo_env_get_rng(mhppo_env *env, uint32_t *mt, int32_t *mti, void *stream);
 
 /* ---- rollout collector (Env_rollout.iterations_rand, Coop-MH-PPO-scalable.py:357-517) ---- */
 
-/* Model_PPO weights of one MLP (Coop-MH-PPO-scalable.py:42-93) in torch layout:
- * W1 [32,in] b1 [32] W2 [64,32] b2 [64] W3 [32,64] b3 [32] W4 [out,32] b4 [out]. */
+/* One Model_PPO MLP (Coop-MH-PPO-scalable.py:42-93), in -> 32 -> 64 -> 32 -> out, ReLU,
+ * packed contiguously in torch layout: W1[32][in] b1[32] W2[64][32] b2[64] W3[32][64]
+ * b3[32] W4[out][32] b4[out] (float32, device).  kind: 0 linear (critic), 1 tanh*std+mean
+ * (continuous actor), 2 pairwise softmax (choice actor). */
 typedef struct mhppo_mlp {
-    const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4;
-    int32_t n_in, n_out;
+    const float *packed;
+    int32_t n_in, n_out, kind, reserved;
+    float mean, std;
 } mhppo_mlp;
 
-/* t=0 choice features, obs_car_ped_d (Coop-MH-PPO-scalable.py:574-611): feat_d float32
- * [N, S, P, dc]; closest ped per slot (closest_ped_d :614-627): int32 [N, S]. */
-int mhppo_featurize_choice(mhppo_env *env, float *feat_d, int32_t *closest, void *stream);
+/* Per-iteration rollout buffers for N envs, S slots, P peds, T steps (device, caller-owned).
+ * Shapes: feat_d [N,S,P,dc] f32, probs_d [N,S,P,2] f32, a_d [N,S,P] i32, logp_d [N,S,P] f32,
+ * closest [N,S] i32, feat_c [N,S,P,13] f32, out_c [N,S,P] f32, obs [N,obs_dim] f32 (current
+ * observation), obs_c [N,S,T,13] f32, act [N,S,T] f32, logp [N,S,T] f32, rew [N,S,T] f64,
+ * ep_min [N,S] f64, exist [N,S] u8. */
+typedef struct mhppo_rollout_bufs {
+    float *feat_d, *probs_d, *logp_d;
+    int32_t *a_d, *closest;
+    float *feat_c, *out_c, *obs;
+    float *obs_c, *act, *logp;
+    double *rew, *ep_min;
+    uint8_t *exist;
+    int32_t T, reserved;
+} mhppo_rollout_bufs;
+
 int mhppo_choice_dim(const mhppo_env *env);
 
-/* Choice head forward + Categorical sample for every (env, slot, ped)
- * (:403-428).  u: float32 [N,S,P] uniforms (parity replay or Philox draws);
- * outputs a_d int32 [N,S,P], logp_d float32 [N,S,P], probs float32 [N,S,P,2]. */
-int mhppo_choice_sample(mhppo_env *env, const mhppo_mlp *actor_choice, const float *feat_d,
-                        const float *u, int32_t *a_d, float *logp_d, float *probs, void *stream);
+/* Episode start (:377-428): reset every env, write obs, choice features obs_car_ped_d
+ * (:574-611) and closest pedestrian (:614-627), run the choice actor and draw
+ * Categorical samples.  When `forced_a` (int32 [N,S,P]) is non-NULL the draws are
+ * replayed from it (parity mode); otherwise u (float32 [N,S,P] uniforms) picks
+ * a = (u >= p0/(p0+p1)). */
+int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const float *u,
+                        const int32_t *forced_a, mhppo_rollout_bufs *bufs, void *stream);
 
-/* One fused rollout step (:430-461): obs_car_ped features for every (slot, ped),
- * cross/wait head forward selected by action_d, min over existing peds, MVN(loc, 0.5)
- * sample from eps float32 [N,S], env step, episodic min of reward_light.
- * Writes step t of the rollout buffers: obs_c float32 [N,S,T,13], act float32 [N,S,T],
- * logp float32 [N,S,T], rew float64 [N,S,T]; updates ep_min float64 [N,S]. */
+/* Step t (:430-461): obs_car_ped features for every (slot, ped) (:541-572), cross/wait
+ * actor chosen by action_d (:440-445), min over pedestrians, MVN(loc, 0.5) sample from
+ * eps (float32 [N,S] standard normals), env.step, episodic min of reward_light (:461). */
 int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
-                       const int32_t *action_d, const int32_t *light_d, const float *eps, int t,
-                       int T, float *obs_c, float *act, float *logp, double *rew, double *ep_min,
-                       void *stream);
+                       const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
+/* The two launches of mhppo_rollout_step, separately (for per-kernel timing):
+ * policy = features + actor forward per (env, slot, ped); sample_env = per-env
+ * min/sample/buffers + env.step + episodic min. */
+int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                         mhppo_rollout_bufs *bufs, void *stream);
+int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
 
-/* Philox-4x32-10 noise for the rollout (perf mode): normal eps [n] and uniforms [n],
- * counter = (seed, offset + i). */
+/* Philox-4x32-10 noise (perf mode): out[i] for counter (offset + i) under key `seed`. */
 int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
 int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
 
 /* ---- returns / advantage / PPO losses (futur_rewards :658-684, train_model_c/_d :778-851) ---- */
 
-/* Segmented reverse discounted scan: G_t = r_t + gamma*G_{t+1} in float64, one segment
- * of T per row; rew float64 [B, T] -> ret float32 [B, T]. */
+/* Segmented reverse discounted scan, G_t = r_t + gamma*G_{t+1} in float64, one segment of
+ * T per row: rew float64 [B,T] -> ret float32 [B,T]. */
 int mhppo_returns_scan(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream);
 
-/* Advantage A = G - V, then (A - mean) / (std_unbiased + 1e-10) over M rows.
- * stats float64 [3] receives (sum A, sum A^2, M) — partial sums when `local_only`
- * (multi-GPU: all-reduce then call mhppo_adv_normalize). */
+/* Advantage statistics of A = G - V over M rows: stats float64 [2] += (sum A, sum A^2)
+ * (caller zeroes it; partial sums all-reduce across ranks).  Normalisation
+ * A' = (A - mean) / (std_unbiased + 1e-10) with mean/std from (stats, M_global). */
 int mhppo_adv_stats(const float *ret, const float *value, int64_t M, double *stats, void *stream);
 int mhppo_adv_normalize(const float *ret, const float *value, int64_t M, const double *stats,
-                        float *adv, void *stream);
+                        double m_global, float *adv, void *stream);
 
-/* Continuous PPO clip surrogate (:795-806): logp = MVN(mu, 0.5).log_prob(act),
- * ratio = exp(logp - logp_old) in float64, L = mean(-min(r A, clip(r, .8, 1.2) A)).
- * Writes dL/dmu float32 [M] (already scaled by 1/M_global) and loss_sum float64 [1]. */
-int mhppo_ppo_cont_fwd_bwd(const float *mu, const float *act, const double *logp_old,
+/* Continuous PPO clip surrogate (:795-806): logp = MVN(mu, 0.5).log_prob(act) (float32),
+ * ratio = exp(logp - logp_old) in float64, L = mean(-min(r A, clamp(r, .8, 1.2) A)).
+ * dmu float32 [M] = dL/dmu with the 1/M_global factor (inv_m); loss float64 [1] += sum. */
+int mhppo_ppo_cont_fwd_bwd(const float *mu, const float *act, const float *logp_old,
                            const float *adv, int64_t M, double inv_m, float *dmu,
-                           double *loss_sum, void *stream);
+                           double *loss, void *stream);
 
-/* Choice PPO surrogate over the reference's M x M broadcast (:834-842) in its exact
- * O(M) form: L = (1/M^2) sum_j [n0 f(r_j0, A_j) + n1 f(r_j1, A_j)].  probs float32
- * [M,2] (softmax outputs), counts int64 [2] = (n0, n1).  Writes dL/dprobs [M,2]. */
-int mhppo_ppo_choice_fwd_bwd(const float *probs, const double *logp_old, const float *adv,
+/* Choice PPO surrogate over the reference's M x M broadcast (:834-842) in its exact O(M)
+ * form L = (1/M^2) sum_j [n0 f(r_j0, A_j) + n1 f(r_j1, A_j)], f(r,A) = -min(rA, clip(r)A),
+ * r_jk = exp(log clamp(p_jk/(p_j0+p_j1)) - logp_old_j).  probs float32 [M,2] (softmax
+ * outputs); counts float64 [2] = (n0, n1) global.  dprobs float32 [M,2] = dL/dprobs. */
+int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const float *adv,
                              int64_t M, const double *counts, double inv_m2, float *dprobs,
-                             double *loss_sum, void *stream);
+                             double *loss, void *stream);
 
-/* Critic MSE (:808-809): loss_sum = sum (V-G)^2, dV = 2 (V-G) * inv_m. */
+/* Critic MSE (:808-809): loss += sum (V-G)^2, dV = 2 (V-G) * inv_m. */
 int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv,
-                      double *loss_sum, void *stream);
+                      double *loss, void *stream);
 
 const char *mhppo_last_error(void);
 const char *mhppo_version(void);

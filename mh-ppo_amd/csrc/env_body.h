@@ -196,12 +196,12 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
 }
 
 // ------------------------------------------------------------------ step
+// act: this env's [2S] actions; rw/rl: this env's [S] outputs (nullable)
 template <int V>
-MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *actions, float *obs, double *rew,
-                           double *rlight, uint8_t *done) {
+MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act, float *obs, double *rw,
+                           double *rl, uint8_t *done) {
   Env<V> E(c, b, e);
   const int nS = c.nS;
-  const double *act = actions + (size_t)e * 2 * nS;
   double time = b.envd[E_TIME * c.N + e];
   double prev[MAXS];
   for (int i = 0; i < nS; i++) prev[i] = E.car(C_SC, i);
@@ -233,10 +233,8 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
     ped_detection<V, MAXS>(E, q, prev, acc, add);
     E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
   }
-  double *rl = rlight + (size_t)e * nS;
-  double *rw = rew + (size_t)e * nS;
   for (int i = 0; i < nS; i++) {
-    if (rlight) rl[i] = acc[i];
+    if (rl) rl[i] = acc[i];
     double Vc = E.car(C_VC, i);
     double r = car_reward(Vc);
     if (E.car(C_LIGHT, i) > 0.0) {
@@ -253,7 +251,7 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
       }
       if (have) r += mn;
     }
-    if (rew) rw[i] = r;
+    if (rw) rw[i] = r;
   }
   env_observe(E, 1, obs);
   int d = (time >= c.ep_len) || (b.envi[EI_PEDTRAF * c.N + e] <= 0);

@@ -28,7 +28,9 @@ template <int V>
 __global__ void __launch_bounds__(TPB)
     k_env_step(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
   int e = blockIdx.x * TPB + threadIdx.x;
-  if (e < c.N) env_step_one<V>(c, b, e, actions, obs, rew, rlight, done);
+  if (e < c.N)
+    env_step_one<V>(c, b, e, actions + (size_t)e * 2 * c.nS, obs, rew ? rew + (size_t)e * c.nS : nullptr,
+                    rlight ? rlight + (size_t)e * c.nS : nullptr, done);
 }
 
 __global__ void __launch_bounds__(TPB) k_env_seed(Cfg c, Bufs b) {

@@ -1,0 +1,505 @@
+// rollout.hip — GPU rollout collector, returns scan and PPO loss kernels (+ C-ABI).
+//
+// Per PPO iteration (Env_rollout.iterations_rand + Algo_PPO.train,
+// Coop-MH-PPO-scalable.py:357-517, :658-684, :778-917), for N envs at once:
+//   begin:  env reset -> choice features -> choice actor -> Categorical draw
+//   step t: [k_policy] one lane per (env, slot, ped): obs_car_ped features and
+//           the cross/wait actor picked by action_d, weights staged in LDS;
+//           [k_sample_env] one lane per env: min over pedestrians, MVN draw,
+//           log-prob, rollout-buffer writes, then the env step itself (the same
+//           env_step_one the standalone step kernel runs) and the episodic min.
+//   end:    reverse discounted scan per (env, slot) segment.
+// Update-time kernels (advantage stats/normalise, PPO surrogates, MSE) are
+// elementwise + deterministic two-pass reductions (fixed summation order).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include "../../include/mhppo.h"
+#include "common.h"
+#include "env_body.h"
+#include "rollout_dev.h"
+
+using namespace mhppo;
+
+namespace mhppo {
+const Cfg &env_cfg(const mhppo_env *env);
+const Bufs &env_bufs(const mhppo_env *env);
+}  // namespace mhppo
+
+namespace {
+constexpr int TPB = 256;
+
+__device__ inline void stage_weights(float *lds, const float *W, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) lds[i] = W[i];
+  __syncthreads();
+}
+
+// -------------------------------------------------------------- begin
+// one lane per (env, slot, ped): choice features, choice actor, Categorical draw
+template <int V>
+__global__ void __launch_bounds__(TPB)
+    k_choice(Cfg c, mhppo_mlp m, const float *u, const int32_t *forced, mhppo_rollout_bufs B) {
+  extern __shared__ float lds[];
+  stage_weights(lds, m.packed, mlp_size(m.n_in, 2));
+  const ObsLayout L = obs_layout(c);
+  const int dc = choice_dim(c);
+  size_t r = (size_t)blockIdx.x * TPB + threadIdx.x;
+  size_t R = (size_t)c.N * c.nS * c.P;
+  if (r >= R) return;
+  int p = (int)(r % c.P), i = (int)((r / c.P) % c.nS);
+  size_t e = r / ((size_t)c.P * c.nS);
+  const float *o = B.obs + e * L.obs_dim;
+  float *f = B.feat_d + r * dc;
+  obs_car_ped_d(o, L, i, p, f);
+  if (p == 0) {
+    B.closest[e * c.nS + i] = closest_ped_d(o, L, i);
+    B.exist[e * c.nS + i] = L.scalable ? (uint8_t)(o[i * L.cw + 6] != 0.0f) : (uint8_t)1;
+  }
+  float pr[2];
+  mlp_forward<0, 2>(lds, dc, f, pr);
+  // Softmax over the pair (Model_PPO type 2, :81-85)
+  float mx = pr[0] > pr[1] ? pr[0] : pr[1];
+  float e0 = expf(pr[0] - mx), e1 = expf(pr[1] - mx);
+  float s = e0 + e1;
+  float p0 = e0 / s, p1 = e1 / s;
+  B.probs_d[r * 2] = p0;
+  B.probs_d[r * 2 + 1] = p1;
+  // Categorical(probs): normalise, clamp to [eps, 1-eps], log (torch/distributions/utils.py)
+  float sum = p0 + p1;
+  float n0 = p0 / sum, n1 = p1 / sum;
+  int a = forced ? forced[r] : (u[r] >= n0 ? 1 : 0);
+  const float eps = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
+  float pn = a ? n1 : n0;
+  pn = pn < eps ? eps : (pn > hi ? hi : pn);
+  B.a_d[r] = a;
+  B.logp_d[r] = logf(pn);
+}
+
+// -------------------------------------------------------------- step
+// one lane per (env, slot, ped): obs_car_ped features + cross/wait actor
+template <int V>
+__global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp mw, mhppo_rollout_bufs B) {
+  extern __shared__ float lds[];
+  const int sz = mlp_size(NF_C, 1);
+  for (int i = threadIdx.x; i < sz; i += blockDim.x) {
+    lds[i] = mc.packed[i];
+    lds[sz + i] = mw.packed[i];
+  }
+  __syncthreads();
+  const ObsLayout L = obs_layout(c);
+  size_t r = (size_t)blockIdx.x * TPB + threadIdx.x;
+  size_t R = (size_t)c.N * c.nS * c.P;
+  if (r >= R) return;
+  int p = (int)(r % c.P), i = (int)((r / c.P) % c.nS);
+  size_t e = r / ((size_t)c.P * c.nS);
+  const float *o = B.obs + e * L.obs_dim;
+  float f[NF_C];
+  float ex = obs_car_ped(o, L, i, p, f);
+  float *fo = B.feat_c + r * NF_C;
+#pragma unroll
+  for (int k = 0; k < NF_C; k++) fo[k] = f[k];
+  if (L.scalable && ex == 0.0f) return;  // `if exist:` gate of the scalable driver (:439)
+  // action_d = 2*a - 1; cross head when action_d <= 0 (:440-445)
+  bool wait = (2 * B.a_d[r] - 1) > 0;
+  const float *W = wait ? lds + sz : lds;
+  const mhppo_mlp &m = wait ? mw : mc;
+  float out;
+  mlp_forward<NF_C, 1>(W, NF_C, f, &out);
+  // Model_PPO type 1: tanh(x) * std + mean (:87-89), two roundings
+  float t = tanhf(out) * m.std;
+  B.out_c[r] = t + m.mean;
+}
+
+// one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min
+template <int V>
+__global__ void __launch_bounds__(TPB)
+    k_sample_env(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  if (e >= c.N) return;
+  const ObsLayout L = obs_layout(c);
+  const int S = c.nS, P = c.P, T = B.T;
+  double act[2 * MAXS], rw[MAXS], rl[MAXS];
+  const float *o = B.obs + (size_t)e * L.obs_dim;
+  for (int i = 0; i < S; i++) {
+    size_t row0 = ((size_t)e * S + i) * P;
+    float loc = 2.0f;  // torch.tensor(car_b[1,0]) (:435)
+    int sel = 0;
+    for (int p = 0; p < P; p++) {
+      if (L.scalable && o[L.ped_off + p * 9 + 7] == 0.0f) continue;
+      float out = B.out_c[row0 + p];
+      loc = t_minimum(loc, out);
+      if (out == loc) sel = p;
+    }
+    float z = eps[(size_t)e * S + i];
+    float a = loc + MVN_L * z;
+    size_t bt = ((size_t)e * S + i) * T + t;
+    B.act[bt] = a;
+    B.logp[bt] = mvn_logp(a, loc);
+    const float *fs = B.feat_c + (row0 + sel) * NF_C;
+    float *fo = B.obs_c + bt * NF_C;
+#pragma unroll
+    for (int k = 0; k < NF_C; k++) fo[k] = fs[k];
+    act[i] = (double)a;
+    int cp = B.closest[(size_t)e * S + i];
+    act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
+  }
+  env_step_one<V>(c, eb, e, act, B.obs, rw, rl, nullptr);
+  for (int i = 0; i < S; i++) {
+    size_t bt = ((size_t)e * S + i) * T + t;
+    B.rew[bt] = rw[i];
+    double m = B.ep_min[(size_t)e * S + i];
+    double x = rl[i];
+    // np.minimum: NaN-propagating
+    B.ep_min[(size_t)e * S + i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_fill_f64(double *p, size_t n, double v) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// --------------------------------------------------------------- noise
+__global__ void __launch_bounds__(TPB) k_philox(uint64_t seed, uint64_t off, float *out, int64_t n, int normal) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  uint64_t ctr = off + (uint64_t)i;
+  uint32_t c4[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x6d687070u, 0u};
+  philox(c4, (uint32_t)seed, (uint32_t)(seed >> 32));
+  if (normal) {
+    float u1 = ((float)(c4[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+    float u2 = (float)(c4[1] >> 8) * (1.0f / 16777216.0f);
+    out[i] = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
+  } else {
+    out[i] = (float)(c4[0] >> 8) * (1.0f / 16777216.0f);
+  }
+}
+
+// ------------------------------------------------------------ returns
+// futur_rewards (:668-672): episodic_reward = rew + 0.99*episodic_reward, float64,
+// then torch.tensor(..., dtype=float) -> float32
+__global__ void __launch_bounds__(TPB) k_returns(const double *rew, float *ret, int64_t B, int T, double gamma) {
+  int64_t b = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (b >= B) return;
+  const double *r = rew + b * T;
+  float *o = ret + b * T;
+  double g = 0.0;
+  for (int t = T - 1; t >= 0; t--) {
+    g = r[t] + gamma * g;
+    o[t] = (float)g;
+  }
+}
+
+// ------------------------------------------------- deterministic reductions
+// Pass 1 writes one partial per block (fixed in-block tree order); pass 2 sums the
+// partials in index order into out[k] (+=).  NP = partial arrays per call.
+template <int NP>
+__device__ inline void block_reduce_store(double (&v)[NP], double *partials, int nblocks) {
+  __shared__ double sh[NP][TPB];
+#pragma unroll
+  for (int k = 0; k < NP; k++) sh[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+#pragma unroll
+      for (int k = 0; k < NP; k++) sh[k][threadIdx.x] += sh[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < NP; k++) partials[(size_t)k * nblocks + blockIdx.x] = sh[k][0];
+}
+
+__global__ void __launch_bounds__(TPB) k_sum_partials(const double *partials, int nblocks, int np, double *out) {
+  int k = threadIdx.x;
+  if (k >= np) return;
+  double s = 0.0;
+  for (int b = 0; b < nblocks; b++) s += partials[(size_t)k * nblocks + b];
+  out[k] += s;
+}
+
+__global__ void __launch_bounds__(TPB) k_adv_stats(const float *ret, const float *val, int64_t M, double *partials) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double v[2] = {0.0, 0.0};
+  if (i < M) {
+    float a = ret[i] - val[i];  // rtgs_batch - V_batch (float32, :786)
+    v[0] = a;
+    v[1] = (double)a * (double)a;
+  }
+  block_reduce_store<2>(v, partials, gridDim.x);
+}
+
+// (A - mean) / (std + 1e-10), torch.std unbiased (:787)
+__global__ void __launch_bounds__(TPB)
+    k_adv_norm(const float *ret, const float *val, int64_t M, const double *stats, double mg, float *adv) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= M) return;
+  double mean = stats[0] / mg;
+  double var = (stats[1] - stats[0] * mean) / (mg - 1.0);
+  float meanf = (float)mean, stdf = (float)sqrt(var > 0 ? var : 0.0);
+  float a = ret[i] - val[i];
+  adv[i] = (a - meanf) / (stdf + 1e-10f);
+}
+
+// d/dr of -min(r A, clamp(r, .8, 1.2) A) with torch's tie rule (minimum splits the
+// gradient evenly on ties; clamp passes it on [0.8, 1.2] inclusive)
+__device__ inline double surr_and_grad(double r, double A, double &dfdr) {
+  double rc = r < 0.8 ? 0.8 : (r > 1.2 ? 1.2 : r);
+  double s1 = r * A, s2 = rc * A;
+  double in = (r >= 0.8 && r <= 1.2) ? 1.0 : 0.0;
+  double g;
+  if (s1 < s2) g = A;
+  else if (s2 < s1) g = in * A;
+  else g = 0.5 * A + 0.5 * in * A;
+  dfdr = -g;
+  return -(s1 < s2 ? s1 : s2);
+}
+
+__global__ void __launch_bounds__(TPB)
+    k_ppo_cont(const float *mu, const float *act, const float *lp_old, const float *adv, int64_t M, double inv_m,
+               float *dmu, double *partials) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double v[1] = {0.0};
+  if (i < M) {
+    // log_prob(action f64) (:800): diff in float64 then float32 solve, float32 tail
+    float diff = (float)((double)act[i] - (double)mu[i]);
+    float x = diff * MVN_INV_L;
+    float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
+    double r = exp((double)lp - (double)lp_old[i]);  // float64 ratio (:803)
+    double dfdr;
+    double f = surr_and_grad(r, (double)adv[i], dfdr);
+    v[0] = f;
+    // dlogp/dmu = x / L  (d/dmu of -0.5 ((a - mu)/L)^2)
+    dmu[i] = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+  }
+  block_reduce_store<1>(v, partials, gridDim.x);
+}
+
+// O(M) form of the M x M Categorical broadcast (:834-842)
+__global__ void __launch_bounds__(TPB)
+    k_ppo_choice(const float *probs, const float *lp_old, const float *adv, int64_t M, const double *counts,
+                 double inv_m2, float *dprobs, double *partials) {
+  int64_t j = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double v[1] = {0.0};
+  if (j < M) {
+    const float eps = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
+    float p0 = probs[2 * j], p1 = probs[2 * j + 1];
+    float s = p0 + p1;
+    float pn[2] = {p0 / s, p1 / s};
+    double A = adv[j], old = lp_old[j];
+    double dlp[2];
+    double f = 0.0;
+    for (int k = 0; k < 2; k++) {
+      float pc = pn[k] < eps ? eps : (pn[k] > hi ? hi : pn[k]);
+      float lp = logf(pc);
+      double r = exp((double)lp - old);
+      double dfdr;
+      double fk = surr_and_grad(r, A, dfdr);
+      f += counts[k] * fk;
+      double pass = (pn[k] >= eps && pn[k] <= hi) ? 1.0 : 0.0;
+      dlp[k] = inv_m2 * counts[k] * dfdr * r * pass / (double)pc;  // dL/dpn_k
+    }
+    v[0] = f;
+    // pn_k = p_k / (p0 + p1)
+    double sd = (double)s;
+    double g0 = (dlp[0] * (1.0 - pn[0]) - dlp[1] * pn[1]) / sd;
+    double g1 = (dlp[1] * (1.0 - pn[1]) - dlp[0] * pn[0]) / sd;
+    dprobs[2 * j] = (float)g0;
+    dprobs[2 * j + 1] = (float)g1;
+  }
+  block_reduce_store<1>(v, partials, gridDim.x);
+}
+
+__global__ void __launch_bounds__(TPB)
+    k_mse(const float *val, const float *ret, int64_t M, double inv_m, float *dv, double *partials) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double v[1] = {0.0};
+  if (i < M) {
+    float d = val[i] - ret[i];
+    v[0] = (double)d * (double)d;
+    dv[i] = (float)(2.0 * inv_m * (double)d);
+  }
+  block_reduce_store<1>(v, partials, gridDim.x);
+}
+
+// scratch for partial sums (per device, grown on demand, stream-ordered use)
+struct Scratch {
+  double *p = nullptr;
+  size_t n = 0;
+};
+Scratch g_scratch[16];
+
+double *scratch(size_t n) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  Scratch &s = g_scratch[dev & 15];
+  if (s.n < n) {
+    if (s.p) (void)hipFree(s.p);
+    if (hipMalloc(&s.p, n * sizeof(double)) != hipSuccess) {
+      s.p = nullptr;
+      s.n = 0;
+      return nullptr;
+    }
+    s.n = n;
+  }
+  return s.p;
+}
+
+#define VLAUNCH(kern, variant, grid, shm, stream, ...)                                                       \
+  do {                                                                                                       \
+    switch (variant) {                                                                                       \
+      case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
+      case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;     \
+      case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break; \
+      default: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;           \
+    }                                                                                                        \
+  } while (0)
+
+inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + TPB - 1) / TPB)); }
+
+}  // namespace
+
+extern "C" {
+
+int mhppo_choice_dim(const mhppo_env *env) { return env ? choice_dim(env_cfg(env)) : MHPPO_EINVAL; }
+
+int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const float *u, const int32_t *forced_a,
+                        mhppo_rollout_bufs *bufs, void *stream) {
+  if (!env || !actor_choice || !bufs || (!u && !forced_a)) return set_error(MHPPO_EINVAL, "null argument");
+  const Cfg &c = env_cfg(env);
+  if (actor_choice->n_in != choice_dim(c) || actor_choice->n_out != 2)
+    return set_error(MHPPO_EINVAL, "choice actor must be %d -> 2 (got %d -> %d)", choice_dim(c), actor_choice->n_in,
+                     actor_choice->n_out);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = mhppo_env_reset(env, bufs->obs, stream);
+  if (rc) return rc;
+  size_t R = (size_t)c.N * c.nS * c.P;
+  size_t shm = sizeof(float) * mlp_size(actor_choice->n_in, 2);
+  VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, *actor_choice, u, forced_a, *bufs);
+  size_t NS = (size_t)c.N * c.nS;
+  hipLaunchKernelGGL(k_fill_f64, grid_for(NS), dim3(TPB), 0, s, bufs->ep_min, NS, 0.0);  // np.array([0.]*S) (:383)
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                         mhppo_rollout_bufs *bufs, void *stream) {
+  if (!env || !actor_cross || !actor_wait || !bufs) return set_error(MHPPO_EINVAL, "null argument");
+  if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
+    return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
+  const Cfg &c = env_cfg(env);
+  size_t R = (size_t)c.N * c.nS * c.P;
+  size_t shm = 2 * sizeof(float) * mlp_size(NF_C, 1);
+  VLAUNCH(k_policy, c.variant, grid_for(R), shm, (hipStream_t)stream, c, *actor_cross, *actor_wait, *bufs);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
+  if (!env || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
+  if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
+  const Cfg &c = env_cfg(env);
+  VLAUNCH(k_sample_env, c.variant, grid_for(c.N), 0, (hipStream_t)stream, c, env_bufs(env), eps, t, *bufs);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait, const float *eps,
+                       int t, mhppo_rollout_bufs *bufs, void *stream) {
+  int rc = mhppo_rollout_policy(env, actor_cross, actor_wait, bufs, stream);
+  if (rc) return rc;
+  return mhppo_rollout_sample_env(env, eps, t, bufs, stream);
+}
+
+int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream) {
+  if (!out || n < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (n == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_philox, grid_for(n), dim3(TPB), 0, (hipStream_t)stream, seed, offset, out, n, 1);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream) {
+  if (!out || n < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (n == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_philox, grid_for(n), dim3(TPB), 0, (hipStream_t)stream, seed, offset, out, n, 0);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_returns_scan(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream) {
+  if (!rew || !ret || B < 0 || T <= 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (B == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_returns, grid_for(B), dim3(TPB), 0, (hipStream_t)stream, rew, ret, B, T, gamma);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_adv_stats(const float *ret, const float *value, int64_t M, double *stats, void *stream) {
+  if (!ret || !value || !stats || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (M == 0) return MHPPO_OK;
+  dim3 g = grid_for(M);
+  double *part = scratch(2 * (size_t)g.x);
+  if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_adv_stats, g, dim3(TPB), 0, s, ret, value, M, part);
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(TPB), 0, s, part, (int)g.x, 2, stats);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_adv_normalize(const float *ret, const float *value, int64_t M, const double *stats, double m_global,
+                        float *adv, void *stream) {
+  if (!ret || !value || !stats || !adv || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (M == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_adv_norm, grid_for(M), dim3(TPB), 0, (hipStream_t)stream, ret, value, M, stats, m_global,
+                     adv);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_ppo_cont_fwd_bwd(const float *mu, const float *act, const float *logp_old, const float *adv, int64_t M,
+                           double inv_m, float *dmu, double *loss, void *stream) {
+  if (!mu || !act || !logp_old || !adv || !dmu || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (M == 0) return MHPPO_OK;
+  dim3 g = grid_for(M);
+  double *part = scratch(g.x);
+  if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_ppo_cont, g, dim3(TPB), 0, s, mu, act, logp_old, adv, M, inv_m, dmu, part);
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(TPB), 0, s, part, (int)g.x, 1, loss);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const float *adv, int64_t M,
+                             const double *counts, double inv_m2, float *dprobs, double *loss, void *stream) {
+  if (!probs || !logp_old || !adv || !counts || !dprobs || !loss || M < 0)
+    return set_error(MHPPO_EINVAL, "bad argument");
+  if (M == 0) return MHPPO_OK;
+  dim3 g = grid_for(M);
+  double *part = scratch(g.x);
+  if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_ppo_choice, g, dim3(TPB), 0, s, probs, logp_old, adv, M, counts, inv_m2, dprobs, part);
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(TPB), 0, s, part, (int)g.x, 1, loss);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv, double *loss,
+                      void *stream) {
+  if (!value || !ret || !dv || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (M == 0) return MHPPO_OK;
+  dim3 g = grid_for(M);
+  double *part = scratch(g.x);
+  if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_mse, g, dim3(TPB), 0, s, value, ret, M, inv_m, dv, part);
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(TPB), 0, s, part, (int)g.x, 1, loss);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+}  // extern "C"

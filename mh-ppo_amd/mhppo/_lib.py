@@ -26,8 +26,14 @@ class EnvCfg(ctypes.Structure):
 
 
 class Mlp(ctypes.Structure):
-    _fields_ = [("w1", P), ("b1", P), ("w2", P), ("b2", P), ("w3", P), ("b3", P), ("w4", P), ("b4", P),
-                ("n_in", I32), ("n_out", I32)]
+    _fields_ = [("packed", P), ("n_in", I32), ("n_out", I32), ("kind", I32), ("reserved", I32),
+                ("mean", ctypes.c_float), ("std", ctypes.c_float)]
+
+
+class RolloutBufs(ctypes.Structure):
+    _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
+                ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
+                ("rew", P), ("ep_min", P), ("exist", P), ("T", I32), ("reserved", I32)]
 
 
 # name: (restype, argtypes)
@@ -41,6 +47,20 @@ _SIGS = {
     "mhppo_env_step": (I32, [P, P, P, P, P, P, P]),
     "mhppo_env_get_state": (I32, [P, P, P]),
     "mhppo_env_get_rng": (I32, [P, P, P, P]),
+    "mhppo_choice_dim": (I32, [P]),
+    "mhppo_rollout_begin": (I32, [P, ctypes.POINTER(Mlp), P, P, ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_rollout_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), P, I32,
+                                 ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_rollout_policy": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
+    "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
+    "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),
+    "mhppo_adv_stats": (I32, [P, P, I64, P, P]),
+    "mhppo_adv_normalize": (I32, [P, P, I64, P, F64, P, P]),
+    "mhppo_ppo_cont_fwd_bwd": (I32, [P, P, P, P, I64, F64, P, P, P]),
+    "mhppo_ppo_choice_fwd_bwd": (I32, [P, P, P, I64, P, F64, P, P, P]),
+    "mhppo_mse_fwd_bwd": (I32, [P, P, I64, F64, P, P, P]),
     "mhppo_last_error": (ctypes.c_char_p, []),
     "mhppo_version": (ctypes.c_char_p, []),
 }

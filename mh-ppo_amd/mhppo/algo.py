@@ -1,0 +1,229 @@
+"""Env_rollout / Algo_PPO with the reference's API, running on the MI355X path.
+
+Drop-in surface of Coop-MH-PPO-scalable.py §3-§4 (:96-1001) and the coop
+driver (Coop-MH-PPO.ipynb cell 0): same class names, constructor arguments,
+method names, hyper-parameter defaults and checkpoint file names/keys.  The
+environment is a VecCrosswalk of N envs: one `train` iteration plays one
+80-step episode in every env (the reference plays 26 episodes of one env for
+batch_size=2048), then runs the same 10 + 10 full-batch epochs.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib, ppo
+from .env import VecCrosswalk
+from .models import Model_PPO
+from .rollout import RolloutGPU, bucket_segments
+
+PREFIX = {"scalable": "pappo-scalable-coop", "coop": "pappo-coop", "4cars": "pappo-coop-4cars", "naif": "pappo-acc6"}
+
+
+def _venv(env):
+    return env.venv if hasattr(env, "venv") else env
+
+
+class Env_rollout:
+    """Batched Env_rollout (:96-684): collects one episode per env per call."""
+
+    def __init__(self, env, nb_cars, max_steps, dt):
+        self.env = _venv(env)
+        self.nb_cars = nb_cars
+        self.dt = dt
+        self.max_steps = max_steps
+        self.shape_env = 2 + 9 + 2
+        self.gpu = RolloutGPU(self.env, T=max_steps)
+        self.shape_env_d = self.gpu.dc
+        self.seed = 0
+        self.iteration = 0
+        self.reset()
+
+    def reset(self):
+        self.batch = None
+        self.cross = self.wait = self.choice = None
+
+    def iterations_rand(self, actor_net_cross, actor_net_wait, actor_net_choice, cov_mat=None, cov_mat_d=None,
+                        batch_size=None, random_rate=0.0, forced_choice=None, eps_tape=None):
+        """One episode in every env (:357-517); buckets the segments like :489-507."""
+        with torch.no_grad():
+            self.batch = self.gpu.collect(actor_net_cross, actor_net_wait, actor_net_choice, seed=self.seed,
+                                          iteration=self.iteration, forced_choice=forced_choice, eps_tape=eps_tape)
+        self.iteration += 1
+        self.cross, self.wait, self.choice = bucket_segments(self.batch)
+        return self.batch
+
+    # reference-named views of the collected batch
+    @property
+    def batch_obs_cross(self):
+        return self.cross["obs"]
+
+    @property
+    def batch_obs_wait(self):
+        return self.wait["obs"]
+
+    @property
+    def batch_obs_choice(self):
+        return self.choice["obs"]
+
+    def futur_rewards(self):
+        """(:658-684) reward-to-go per bucket (float32); choice = episodic min."""
+        return self.cross["ret"], self.wait["ret"], self.choice["ret"]
+
+    def immediate_rewards(self):
+        """(:635-656)"""
+        return self.cross["rew"].float(), self.wait["rew"].float(), self.choice["ret"]
+
+
+class Algo_PPO:
+    """Multi-head PPO (:698-1001)."""
+
+    def __init__(self, policy_class, env, **hyperparameters):
+        self._init_hyperparameters(hyperparameters)
+        venv = _venv(env)
+        self.venv = venv
+        self.max_steps = venv.max_episode
+        S = venv.n_slots
+        if not hasattr(self, "num_states_c"):
+            self.num_states_c = 13
+        if not hasattr(self, "num_states_d"):
+            self.num_states_d = _lib.lib().mhppo_choice_dim(venv.handle)
+        if not hasattr(self, "num_actions"):
+            self.num_actions = 1
+        if not hasattr(self, "mean"):
+            self.mean = (venv.cfg.car_b[2] + venv.cfg.car_b[0]) / 2.0   # :1044
+        if not hasattr(self, "std"):
+            self.std = (venv.cfg.car_b[2] - venv.cfg.car_b[0]) / 2.0    # :1045
+        if not hasattr(self, "dt"):
+            self.dt = venv.dt
+        dev = venv.device
+        self.actor_net_cross = policy_class(self.num_states_c, self.num_actions, 1, nb_car=S, mean=self.mean,
+                                            std=self.std).to(dev)
+        self.actor_net_wait = policy_class(self.num_states_c, self.num_actions, 1, nb_car=S, mean=self.mean,
+                                           std=self.std).to(dev)
+        self.actor_net_choice = policy_class(self.num_states_d, 2, 2).to(dev)
+        self.critic_net_cross = policy_class(self.num_states_c, 1, 0).to(dev)
+        self.critic_net_wait = policy_class(self.num_states_c, 1, 0).to(dev)
+        self.critic_net_choice = policy_class(self.num_states_d, 1, 0).to(dev)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            for net in self.nets():  # replicas start identical (rank 0's init)
+                for p in net.parameters():
+                    dist.broadcast(p.data, src=0)
+        A = torch.optim.Adam
+        self.optimizer_critic_cross = A(self.critic_net_cross.parameters(), self.critic_lr)
+        self.optimizer_critic_wait = A(self.critic_net_wait.parameters(), self.critic_lr)
+        self.optimizer_critic_choice = A(self.critic_net_choice.parameters(), self.critic_d_lr)
+        self.optimizer_actor_cross = A(self.actor_net_cross.parameters(), self.actor_lr)
+        self.optimizer_actor_wait = A(self.actor_net_wait.parameters(), self.actor_lr)
+        self.optimizer_actor_choice = A(self.actor_net_choice.parameters(), self.actor_d_lr)
+        self.value_std = 0.5
+        self.value_std_d = 0.1
+        self.cov_var = torch.full(size=(self.num_actions,), fill_value=self.value_std)
+        self.cov_mat = torch.diag(self.cov_var)
+        self.cov_var_d = torch.full(size=(2 * S,), fill_value=self.value_std_d)
+        self.cov_mat_d = torch.diag(self.cov_var_d)
+        self.rollout = Env_rollout(venv, S, self.max_steps, self.dt)
+        self.rollout.seed = getattr(self, "seed", 0)
+        self.ep_reward_cross, self.ep_reward_wait, self.ep_reward_choice = [], [], []
+        self.ep_scenario_balance = []
+        self.last_losses = {}
+
+    def nets(self):
+        return [self.actor_net_cross, self.actor_net_wait, self.actor_net_choice, self.critic_net_cross,
+                self.critic_net_wait, self.critic_net_choice]
+
+    def _init_hyperparameters(self, hyperparameters):
+        """(:919-933) defaults; overrides set as attributes (the reference uses exec)."""
+        self.num_algo = 1
+        self.total_loop = 0
+        self.batch_size = 2048
+        self.gamma = 0.99
+        self.critic_lr = 1e-3
+        self.actor_lr = 3e-4
+        self.critic_d_lr = 1e-3
+        self.actor_d_lr = 3e-4
+        self.verbose = True
+        for k, v in hyperparameters.items():
+            setattr(self, k, v)
+
+    def update(self):
+        """10 epochs of cross+wait, then 10 epochs of choice (:868-882) on the collected batch."""
+        r = self.rollout
+        dev = self.venv.device
+        c, w, d = r.cross, r.wait, r.choice
+        m_c = ppo.global_count(c["ret"].numel(), dev)
+        m_w = ppo.global_count(w["ret"].numel(), dev)
+        m_d = ppo.global_count(d["ret"].numel(), dev)
+        counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
+        ppo._allreduce_(counts)
+        losses = {}
+        for _ in range(10):
+            if m_c > 0:
+                losses["cross"] = ppo.train_model_c(self.actor_net_cross, self.critic_net_cross,
+                                                    self.optimizer_actor_cross, self.optimizer_critic_cross,
+                                                    c["obs"], c["act"], c["logp"], c["ret"], m_c)
+            if m_w > 0:
+                losses["wait"] = ppo.train_model_c(self.actor_net_wait, self.critic_net_wait,
+                                                   self.optimizer_actor_wait, self.optimizer_critic_wait,
+                                                   w["obs"], w["act"], w["logp"], w["ret"], m_w)
+        for _ in range(10):
+            if m_d > 0:
+                losses["choice"] = ppo.train_model_d(self.actor_net_choice, self.critic_net_choice,
+                                                     self.optimizer_actor_choice, self.optimizer_critic_choice,
+                                                     d["obs"], d["act"], d["logp"], d["ret"], m_d, counts)
+        self.last_losses = {k: (float(a.item()) / (m_d * m_d if k == "choice" else (m_c if k == "cross" else m_w)),
+                                float(b.item()) / (m_d if k == "choice" else (m_c if k == "cross" else m_w)))
+                            for k, (a, b) in losses.items()} if self.verbose else losses
+        return m_c, m_w, m_d
+
+    def train(self, nb_loop):
+        """(:854-917)"""
+        for ep in range(nb_loop):
+            self.rollout.reset()
+            self.rollout.iterations_rand(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
+                                         self.cov_mat, self.cov_mat_d, self.batch_size)
+            m_c, m_w, m_d = self.update()
+            if self.verbose:
+                rc, rw, rd = self.rollout.immediate_rewards()
+                dev = self.venv.device
+                sums = torch.tensor([float(rc.sum()), float(rw.sum()), float(rd.sum())], dtype=torch.float64,
+                                    device=dev)
+                ppo._allreduce_(sums)
+                if m_c > 0:
+                    self.ep_reward_cross.append(float(sums[0]) / (m_c))
+                if m_w > 0:
+                    self.ep_reward_wait.append(float(sums[1]) / (m_w))
+                self.ep_reward_choice.append(float(sums[2]) / max(m_d, 1))
+                self.ep_scenario_balance.append([int(m_c), int(m_w)])
+                print("Episode * {} * And Number of steps is ==> {}".format(ep, ep * self.batch_size))
+                print("Average Cross reward is ==> {}, Average Wait reward is ==> {}".format(
+                    np.mean(self.ep_reward_cross[-10:]) if self.ep_reward_cross else float("nan"),
+                    np.mean(self.ep_reward_wait[-10:]) if self.ep_reward_wait else float("nan")))
+                print("Average Choice reward is ==> {}".format(np.mean(self.ep_reward_choice[-10:])))
+                print("Number Cross is ==> {} and Number Wait is ==> {} ".format(int(m_c), int(m_w)))
+            self.total_loop = self.total_loop + 1
+
+    # --------------------------------------------------------------- checkpoints
+    def _path(self, head, kind, num_algo, total_loop):
+        pre = PREFIX.get(self.venv.variant, "pappo")
+        return "load_model/weights/{}-{}-{:02d}-{}-step-{:03d}0.pth".format(pre, head, num_algo, kind,
+                                                                           int(total_loop / 10))
+
+    def loading(self, num_algo, total_loop):
+        """(:935-955) torch state_dicts, loaded without executing anything from the file."""
+        self.num_algo, self.total_loop = num_algo, total_loop
+        for head in ("cross", "wait", "choice"):
+            for kind in ("actor", "critic"):
+                net = getattr(self, f"{kind}_net_{head}")
+                sd = torch.load(self._path(head, kind, num_algo, total_loop), map_location=self.venv.device,
+                                weights_only=True)
+                net.load_state_dict(sd)
+
+    def saving(self):
+        """(:985-1001)"""
+        os.makedirs("load_model/weights", exist_ok=True)
+        for head in ("cross", "wait", "choice"):
+            for kind in ("actor", "critic"):
+                net = getattr(self, f"{kind}_net_{head}")
+                torch.save(net.state_dict(), self._path(head, kind, self.num_algo, self.total_loop))

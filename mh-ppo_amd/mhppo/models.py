@@ -1,0 +1,79 @@
+"""Model_PPO — the reference's multi-head MLP (Coop-MH-PPO-scalable.py:42-93).
+
+Same constructor signature, same submodule names (`layer1..layer4`, so shipped
+`.pth` state_dicts load), same construction order (so `torch.manual_seed(s)`
+yields the reference's initial weights), same forward.  `packed()` lays the
+weights out contiguously for the HIP rollout kernels (include/mhppo.h mhppo_mlp).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+
+class Model_PPO(nn.Module):
+    """in -> 32 -> 64 -> 32 -> out, ReLU.  model_type 2: pairwise softmax (choice actor);
+    1: tanh * std + mean (continuous actor); 0: linear (critics)."""
+
+    def __init__(self, np_inputs, nb_outputs, model_type=0, nb_car=1, mean=0, std=1):
+        super().__init__()
+        self.model_type = model_type
+        self.nb_car = nb_car
+        self.mean = mean
+        self.std = std
+        self.layer1 = nn.Linear(np_inputs, 32)
+        self.layer2 = nn.Linear(32, 64)
+        self.layer3 = nn.Linear(64, 32)
+        self.layer4 = nn.Linear(32, nb_outputs)
+        # The reference re-creates layer4 for types 2 and 1 (:58-64): keep that RNG use.
+        if self.model_type == 2:
+            self.layer4 = nn.Linear(32, nb_outputs)
+            self.return_layer = nn.Softmax(dim=-1)
+        if self.model_type == 1:
+            self.layer4 = nn.Linear(32, nb_outputs)
+            self.return_layer = nn.Tanh()
+        torch.nn.init.orthogonal_(self.layer4.weight)
+
+    def forward(self, input1):
+        if isinstance(input1, np.ndarray):
+            input1 = torch.tensor(input1, dtype=torch.float, device=self.layer1.weight.device)
+        a1 = F.relu(self.layer1(input1))
+        a2 = F.relu(self.layer2(a1))
+        a3 = F.relu(self.layer3(a2))
+        if self.model_type == 2:
+            out = self.layer4(a3).reshape(-1, 2)
+            return torch.flatten(self.return_layer(out))
+        if self.model_type == 1:
+            out = self.layer4(a3)
+            return torch.add(torch.mul(self.return_layer(out), self.std), self.mean)
+        return self.layer4(a3)
+
+    @property
+    def n_in(self):
+        return self.layer1.in_features
+
+    @property
+    def n_out(self):
+        return self.layer4.out_features
+
+    def packed(self):
+        """Contiguous float32 copy W1 b1 W2 b2 W3 b3 W4 b4 (torch layouts) on the model's device."""
+        parts = []
+        for lay in (self.layer1, self.layer2, self.layer3, self.layer4):
+            parts += [lay.weight.detach().reshape(-1), lay.bias.detach().reshape(-1)]
+        return torch.cat(parts).float().contiguous()
+
+    def mlp_desc(self, packed=None):
+        """(mhppo_mlp struct, backing tensor) for the C-ABI."""
+        t = self.packed() if packed is None else packed
+        d = _lib.Mlp()
+        d.packed = ctypes.c_void_p(t.data_ptr())
+        d.n_in, d.n_out = self.n_in, self.n_out
+        d.kind = self.model_type
+        d.mean = float(self.mean)
+        d.std = float(self.std)
+        return d, t

@@ -1,0 +1,156 @@
+"""GPU rollout collector: one PPO iteration's episodes for N envs at once.
+
+Batched form of `Env_rollout.iterations_rand` (Coop-MH-PPO-scalable.py:357-517;
+coop driver Coop-MH-PPO.ipynb cell 0): every env plays one 80-step episode;
+the choice head is sampled once at t=0 (ped_traffic never changes, so
+`need_new_d` is only true at the start); each step runs the fused
+policy kernel and the fused sample+env-step kernel.  Buffers are laid out
+[env, slot, t], which is exactly the reference's episode-major, car-major,
+time-ascending batch order once segments are bucketed (bucket_segments).
+
+Noise: in perf mode the standard normals (MVN eps) and the Categorical
+uniforms come from Philox keyed by (seed, iteration) with counters built from
+the GLOBAL env id, so a sharded run draws the same noise per env as a single
+GPU.  In parity mode callers pass the reference's recorded draws instead.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+NF_C = 13
+_CTR_STEP = 1 << 40  # counter stride between time steps (global env*slot index below it)
+
+
+class RolloutBatch:
+    """Views of one iteration's rollout buffers (all on the env's device)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class RolloutGPU:
+    def __init__(self, venv, T=None):
+        self.venv = venv
+        self.T = T or venv.max_episode
+        N, S, P = venv.n_envs, venv.n_slots, venv.nb_ped
+        self.N, self.S, self.P = N, S, P
+        self.dc = _lib.lib().mhppo_choice_dim(venv.handle)
+        dev = venv.device
+        f32, f64, i32 = torch.float32, torch.float64, torch.int32
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
+        self.feat_d = z((N, S, P, self.dc), f32)
+        self.probs_d = z((N, S, P, 2), f32)
+        self.logp_d = z((N, S, P), f32)
+        self.a_d = z((N, S, P), i32)
+        self.closest = z((N, S), i32)
+        self.feat_c = z((N, S, P, NF_C), f32)
+        self.out_c = z((N, S, P), f32)
+        self.obs = z((N, venv.obs_dim), f32)
+        self.obs_c = z((N, S, self.T, NF_C), f32)
+        self.act = z((N, S, self.T), f32)
+        self.logp = z((N, S, self.T), f32)
+        self.rew = z((N, S, self.T), f64)
+        self.ep_min = z((N, S), f64)
+        self.exist = z((N, S), torch.uint8)
+        self.eps = z((self.T, N, S), f32)
+        self.u = z((N, S, P), f32)
+        b = _lib.RolloutBufs()
+        for name in ("feat_d", "probs_d", "logp_d", "a_d", "closest", "feat_c", "out_c", "obs", "obs_c", "act",
+                     "logp", "rew", "ep_min", "exist"):
+            setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
+        b.T = self.T
+        self._bufs = b
+
+    def draw_noise(self, seed, iteration):
+        """Philox perf-mode noise for one iteration (global-env-id counters)."""
+        L = _lib.lib()
+        key = (int(seed) * 1000003 + int(iteration)) & 0xFFFFFFFFFFFFFFFF
+        off = int(self.venv.cfg.env_id_offset)
+        st = _lib.stream_ptr()
+        _lib.check(L.mhppo_philox_uniform(key, off * self.S * self.P, _lib.ptr(self.u), self.u.numel(), st))
+        for t in range(self.T):
+            _lib.check(L.mhppo_philox_normal(key, (t + 1) * _CTR_STEP + off * self.S, _lib.ptr(self.eps[t]),
+                                             self.eps[t].numel(), st))
+
+    def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
+                eps_tape=None, step_events=None):
+        """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
+        replay recorded draws (parity mode); otherwise Philox noise is drawn."""
+        L = _lib.lib()
+        if forced_choice is None or eps_tape is None:
+            self.draw_noise(seed, iteration)
+        if eps_tape is not None:
+            self.eps.copy_(eps_tape.to(self.eps.device, torch.float32))
+        fa = None
+        if forced_choice is not None:
+            fa = forced_choice.to(self.a_d.device, torch.int32).contiguous()
+        mc, tc = actor_choice.mlp_desc()
+        mx, tx = actor_cross.mlp_desc()
+        mw, tw = actor_wait.mlp_desc()
+        st = _lib.stream_ptr()
+        _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
+                                         ctypes.byref(self._bufs), st))
+        for t in range(self.T):
+            _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                              ctypes.byref(self._bufs), st))
+            if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
+                step_events[t][0].record()
+            _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
+                                                  ctypes.byref(self._bufs), st))
+            if step_events is not None:
+                step_events[t][1].record()
+        del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
+        return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,
+                            closest=self.closest, obs_c=self.obs_c, act=self.act, logp=self.logp, rew=self.rew,
+                            ep_min=self.ep_min, exist=self.exist, N=self.N, S=self.S, P=self.P, T=self.T)
+
+
+def returns_scan(rew, gamma=0.99):
+    """futur_rewards (:658-684): float64 reverse discounted scan per [.., T] row -> float32."""
+    T = rew.shape[-1]
+    r = rew.reshape(-1, T).contiguous()
+    out = torch.empty(r.shape, dtype=torch.float32, device=rew.device)
+    _lib.check(_lib.lib().mhppo_returns_scan(_lib.ptr(r), _lib.ptr(out), r.shape[0], T, gamma, _lib.stream_ptr()))
+    return out.reshape(rew.shape)
+
+
+def bucket_segments(batch):
+    """Split (env, slot) episode segments into the reference's cross/wait/choice batches.
+
+    Bucket rule (:489-507): only existing cars (scalable driver); cross when
+    action_d[i] <= 0 where action_d is the per-(car, ped) array indexed by the CAR
+    index i.  Choice sample per existing car: the closest pedestrian's
+    features, action and log-prob, reward = episodic min of reward_light.
+    """
+    N, S, P, T = batch.N, batch.S, batch.P, batch.T
+    a_flat = batch.a_d.reshape(N, S * P)
+    action_d_i = 2 * a_flat[:, :S].to(torch.int32) - 1  # action_d[i], i < S
+    exist = batch.exist.bool()
+    cross = exist & (action_d_i <= 0)
+    wait = exist & (action_d_i > 0)
+    seg_cross = torch.nonzero(cross.reshape(-1)).squeeze(1)
+    seg_wait = torch.nonzero(wait.reshape(-1)).squeeze(1)
+    seg_all = torch.nonzero(exist.reshape(-1)).squeeze(1)
+    ret = returns_scan(batch.rew)
+
+    def rows(seg):
+        obs = batch.obs_c.reshape(N * S, T, NF_C).index_select(0, seg).reshape(-1, NF_C)
+        act = batch.act.reshape(N * S, T).index_select(0, seg).reshape(-1)
+        lp = batch.logp.reshape(N * S, T).index_select(0, seg).reshape(-1)
+        rt = ret.reshape(N * S, T).index_select(0, seg).reshape(-1)
+        rw = batch.rew.reshape(N * S, T).index_select(0, seg).reshape(-1)
+        return dict(obs=obs, act=act, logp=lp, ret=rt, rew=rw, n_seg=int(seg.numel()))
+
+    cl = batch.closest.reshape(N * S).long().index_select(0, seg_all)
+    base = seg_all * P + cl
+    dc = batch.feat_d.shape[-1]
+    choice = dict(
+        obs=batch.feat_d.reshape(N * S * P, dc).index_select(0, base),
+        act=batch.a_d.reshape(-1).index_select(0, base),
+        logp=batch.logp_d.reshape(-1).index_select(0, base),
+        ret=batch.ep_min.reshape(-1).index_select(0, seg_all).float(),
+        n_seg=int(seg_all.numel()),
+    )
+    return rows(seg_cross), rows(seg_wait), choice

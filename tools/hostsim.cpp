@@ -42,8 +42,11 @@ void hs_reset(HostEnv *h, float *obs) {
     }
   }
 }
-void hs_step(HostEnv *h, const double *a, float *obs, double *rew, double *rl, uint8_t *done) {
+void hs_step(HostEnv *h, const double *a0, float *obs, double *rew0, double *rl0, uint8_t *done) {
+  const int S = h->c.nS;
   for (int e = 0; e < h->c.N; e++) {
+    const double *a = a0 + (size_t)e * 2 * S;
+    double *rew = rew0 + (size_t)e * S, *rl = rl0 + (size_t)e * S;
     switch (h->c.variant) {
       case V_COOP: env_step_one<V_COOP>(h->c, h->b, e, a, obs, rew, rl, done); break;
       case V_4CARS: env_step_one<V_4CARS>(h->c, h->b, e, a, obs, rew, rl, done); break;
