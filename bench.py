@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--nb-ped", type=int, default=1)
     ap.add_argument("--nb-lines", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-envs", type=int, default=64)
+    ap.add_argument("--cpu-sample-envs", type=int, default=256)
     return ap.parse_args()
 
 

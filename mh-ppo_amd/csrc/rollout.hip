@@ -211,12 +211,20 @@ __device__ inline void block_reduce_store(double (&v)[NP], double *partials, int
     for (int k = 0; k < NP; k++) partials[(size_t)k * nblocks + blockIdx.x] = sh[k][0];
 }
 
+// one block per partial array: each thread sums a fixed strided subset, then a fixed
+// tree — the summation order depends only on nblocks, never on scheduling
 __global__ void __launch_bounds__(TPB) k_sum_partials(const double *partials, int nblocks, int np, double *out) {
-  int k = threadIdx.x;
-  if (k >= np) return;
+  __shared__ double sh[TPB];
+  int k = blockIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nblocks; b++) s += partials[(size_t)k * nblocks + b];
-  out[k] += s;
+  for (int b = threadIdx.x; b < nblocks; b += TPB) s += partials[(size_t)k * nblocks + b];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = TPB / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[k] += sh[0];
 }
 
 __global__ void __launch_bounds__(TPB) k_adv_stats(const float *ret, const float *val, int64_t M, double *partials) {
@@ -444,7 +452,7 @@ int mhppo_adv_stats(const float *ret, const float *value, int64_t M, double *sta
   if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_adv_stats, g, dim3(TPB), 0, s, ret, value, M, part);
-  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(TPB), 0, s, part, (int)g.x, 2, stats);
+  hipLaunchKernelGGL(k_sum_partials, dim3(2), dim3(TPB), 0, s, part, (int)g.x, 2, stats);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

@@ -67,6 +67,20 @@ class Model_PPO(nn.Module):
             parts += [lay.weight.detach().reshape(-1), lay.bias.detach().reshape(-1)]
         return torch.cat(parts).float().contiguous()
 
+    def load_packed(self, flat):
+        """Inverse of packed(): load a flat W1 b1 .. W4 b4 vector into the layers."""
+        flat = torch.as_tensor(flat, dtype=torch.float32).reshape(-1)
+        off = 0
+        with torch.no_grad():
+            for lay in (self.layer1, self.layer2, self.layer3, self.layer4):
+                for p in (lay.weight, lay.bias):
+                    n = p.numel()
+                    p.copy_(flat[off:off + n].view_as(p))
+                    off += n
+        if off != flat.numel():
+            raise ValueError(f"packed size {flat.numel()} != model size {off}")
+        return self
+
     def mlp_desc(self, packed=None):
         """(mhppo_mlp struct, backing tensor) for the C-ABI."""
         t = self.packed() if packed is None else packed

@@ -114,3 +114,118 @@ def rng_stream(seed, kind, n, a=0.0, b=0.0, per=1):
     out = np.zeros(n * per, np.float64)
     k = L.oracle_rng_stream(seed, kind, a, b, n, _p(out))
     return out[:k]
+
+
+def choice_dim(variant, S):
+    return 2 + 6 * (S - 1) + 10 if variant == "scalable" else 2 + 5 * (S - 1) + 10
+
+
+def rollout(variant, nb_car, nb_ped, nb_lines, seeds, w_cross, w_wait, w_choice, mean=-1.0, std=3.0,
+            forced_a=None, u=None, eps=None, T=80):
+    """One oracle episode per seed (Env_rollout.iterations_rand semantics).
+
+    w_*: packed float32 weights (Model_PPO.packed()); forced_a int32 [N,S,P] or u float32 [N,S,P];
+    eps float32 [T,N,S].  Returns dict of numpy arrays laid out like the GPU buffers."""
+    L = lib()
+    P_ = ctypes.c_void_p
+    L.oracle_rollout_episode.restype = ctypes.c_int
+    L.oracle_rollout_episode.argtypes = [P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_, P_,
+                                         ctypes.c_float, ctypes.c_float] + [P_] * 14
+    N = len(seeds)
+    S = 2 * nb_lines if variant == "scalable" else nb_car
+    dc = choice_dim(variant, S)
+    out = dict(feat_d=np.zeros((N, S, nb_ped, dc), np.float32), probs_d=np.zeros((N, S, nb_ped, 2), np.float32),
+               a_d=np.zeros((N, S, nb_ped), np.int32), logp_d=np.zeros((N, S, nb_ped), np.float32),
+               closest=np.zeros((N, S), np.int32), exist=np.zeros((N, S), np.uint8),
+               obs_c=np.zeros((N, S, T, 13), np.float32), act=np.zeros((N, S, T), np.float32),
+               logp=np.zeros((N, S, T), np.float32), rew=np.zeros((N, S, T), np.float64),
+               ep_min=np.zeros((N, S), np.float64))
+    wc, ww, wd = (np.ascontiguousarray(w, np.float32) for w in (w_cross, w_wait, w_choice))
+    eps = np.ascontiguousarray(eps, np.float32)
+    for n, sd in enumerate(seeds):
+        env = OracleEnv(variant, nb_car, nb_ped, nb_lines, seed=int(sd))
+        fa = None if forced_a is None else np.ascontiguousarray(forced_a[n], np.int32)
+        uu = np.ascontiguousarray(u[n] if u is not None else np.zeros((S, nb_ped)), np.float32)
+        ep = np.ascontiguousarray(eps[:, n, :], np.float32)
+        o = {k: np.ascontiguousarray(v[n]) for k, v in out.items()}
+        L.oracle_rollout_episode(env.h, VARIANTS[variant], S, nb_ped, T, _p(wc), _p(ww), _p(wd), mean, std,
+                                 None if fa is None else _p(fa), _p(uu), _p(ep), *[_p(o[k]) for k in (
+                                     "feat_d", "probs_d", "a_d", "logp_d", "closest", "exist", "obs_c", "act",
+                                     "logp", "rew", "ep_min")])
+        for k in out:
+            out[k][n] = o[k]
+    return out
+
+
+_CPU_NETS = {}
+
+
+def _mlp(n_in, n_out, kind):
+    import torch
+    import torch.nn as nn
+
+    class _M(nn.Module):  # Model_PPO restated (Coop-MH-PPO-scalable.py:42-93)
+        def __init__(self):
+            super().__init__()
+            self.layer1, self.layer2 = nn.Linear(n_in, 32), nn.Linear(32, 64)
+            self.layer3, self.layer4 = nn.Linear(64, 32), nn.Linear(32, n_out)
+            nn.init.orthogonal_(self.layer4.weight)
+
+        def forward(self, x):
+            h = torch.relu(self.layer3(torch.relu(self.layer2(torch.relu(self.layer1(x))))))
+            y = self.layer4(h)
+            if kind == 2:
+                return torch.softmax(y.reshape(-1, 2), -1).reshape(-1)
+            if kind == 1:
+                return torch.tanh(y) * 3.0 + (-1.0)
+            return y
+
+        def packed(self):
+            return torch.cat([p.detach().reshape(-1) for l in (self.layer1, self.layer2, self.layer3, self.layer4)
+                              for p in (l.weight, l.bias)]).numpy()
+    return _M()
+
+
+def cpu_iteration(variant, n, nb_car, nb_ped, nb_lines, seed=0):
+    """One full PPO iteration on the CPU: C oracle env + rollout for n envs (1 thread),
+    then 10+10 epochs of the PyTorch-CPU update restatement (oracle/ppo_ref.py)."""
+    import torch
+    from . import ppo_ref
+    S = 2 * nb_lines if variant == "scalable" else nb_car
+    key = (variant, nb_car, nb_ped, nb_lines)
+    if key not in _CPU_NETS:
+        torch.manual_seed(0)
+        dc = choice_dim(variant, S)
+        nets = dict(ac=_mlp(13, 1, 1), aw=_mlp(13, 1, 1), ad=_mlp(dc, 2, 2), cc=_mlp(13, 1, 0), cw=_mlp(13, 1, 0),
+                    cd=_mlp(dc, 1, 0))
+        opts = {k: torch.optim.Adam(v.parameters(), 3e-4 if k[0] == "a" else 1e-3) for k, v in nets.items()}
+        _CPU_NETS[key] = (nets, opts)
+    nets, opts = _CPU_NETS[key]
+    rng = np.random.default_rng(seed)
+    eps = rng.normal(size=(80, n, S)).astype(np.float32)
+    u = rng.uniform(size=(n, S, nb_ped)).astype(np.float32)
+    o = rollout(variant, nb_car, nb_ped, nb_lines, [seed * n + e for e in range(n)], nets["ac"].packed(),
+                nets["aw"].packed(), nets["ad"].packed(), u=u, eps=eps)
+    action_d_i = 2 * o["a_d"].reshape(n, -1)[:, :S] - 1
+    ex = o["exist"].astype(bool) if variant == "scalable" else np.ones((n, S), bool)
+    ret = ppo_ref.returns_scan(torch.tensor(o["rew"].reshape(-1, 80))).reshape(n, S, 80)
+    for head, sel in (("c", ex & (action_d_i <= 0)), ("w", ex & (action_d_i > 0))):
+        if not sel.any():
+            continue
+        obs = torch.tensor(o["obs_c"][sel].reshape(-1, 13))
+        act = torch.tensor(o["act"][sel].reshape(-1))
+        lp = torch.tensor(o["logp"][sel].reshape(-1))
+        rt = ret[torch.tensor(sel)].reshape(-1)
+        a, c = nets["a" + head], nets["c" + head]
+        for _ in range(10):
+            ppo_ref.train_model_c(a, c, opts["a" + head], opts["c" + head], obs, act, lp, rt)
+    idx = np.nonzero(ex.reshape(-1))[0]
+    cl = o["closest"].reshape(-1)[idx]
+    fd = o["feat_d"].reshape(n * S, nb_ped, -1)[idx, cl]
+    ad_ = o["a_d"].reshape(n * S, nb_ped)[idx, cl]
+    lpd = o["logp_d"].reshape(n * S, nb_ped)[idx, cl]
+    rd = o["ep_min"].reshape(-1)[idx].astype(np.float32)
+    for _ in range(10):
+        ppo_ref.train_model_d(nets["ad"], nets["cd"], opts["ad"], opts["cd"], torch.tensor(fd), torch.tensor(ad_),
+                              torch.tensor(lpd), torch.tensor(rd))
+    return n * 80

@@ -40,7 +40,7 @@ def train_model_c(actor, critic, opt_a, opt_c, obs, act, logp_old, rtgs):
     opt_c.zero_grad()
     critic_loss.backward()
     opt_c.step()
-    return float(actor_loss), float(critic_loss)
+    return float(actor_loss.detach()), float(critic_loss.detach())
 
 
 def train_model_d(actor, critic, opt_a, opt_c, obs, act, logp_old, rtgs):
@@ -63,7 +63,7 @@ def train_model_d(actor, critic, opt_a, opt_c, obs, act, logp_old, rtgs):
     opt_c.zero_grad()
     critic_loss.backward()
     opt_c.step()
-    return float(actor_loss), float(critic_loss)
+    return float(actor_loss.detach()), float(critic_loss.detach())
 
 
 def returns_scan(rew_segments, gamma=0.99):
