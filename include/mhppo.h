@@ -72,7 +72,8 @@ int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *re
 
 /* Read back the per-env scalar/attribute view the reference drivers touch
  * (env.cross, ped_traffic, car_traffic, cars[i].exist, pedestrian[j].waiting_time,
- * internal flags): out float64 [N, mhppo_env_state_dim()]. */
+ * internal flags): out float64 [N, mhppo_env_state_dim() = 21P + 8 car slots + 4], laid out
+ * [per ped 20][per car slot 8][cross, time, ped_traffic, car_traffic][per ped exist]. */
 int mhppo_env_state_dim(const mhppo_env *env);
 int mhppo_env_get_state(mhppo_env *env, double *out, void *stream);
 /* RNG cursor: mt uint32 [N, 624], mti int32 [N] (device). */

@@ -269,7 +269,7 @@ MHPPO_HD inline void env_seed_one(const Cfg &c, const Bufs &b, int e) {
 }
 
 // ------------------------------------------------------------- state dump
-// [peds 20P][AV cars 8 nS][followers 8 (nC-nS)][cross, time, ped_traffic, car_traffic]
+// [peds 20P][AV cars 8 nS][followers 8 (nC-nS)][cross, time, ped_traffic, car_traffic][ped exist P]
 template <int V>
 MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int dim) {
   Env<V> E(c, b, e);
@@ -292,6 +292,7 @@ MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int
   o[k++] = b.envd[E_TIME * c.N + e];
   o[k++] = (double)b.envi[EI_PEDTRAF * c.N + e];
   o[k++] = (double)b.envi[EI_CARTRAF * c.N + e];
+  for (int p = 0; p < c.P; p++) o[k++] = (E.pflag(p) & F_EXIST) ? 1.0 : 0.0;
 }
 
 

@@ -124,7 +124,7 @@ void mhppo_env_destroy(mhppo_env *env) {
 
 int mhppo_env_obs_dim(const mhppo_env *env) { return env ? env->c.obs_dim : MHPPO_EINVAL; }
 int mhppo_env_slots(const mhppo_env *env) { return env ? env->c.nS : MHPPO_EINVAL; }
-int mhppo_env_state_dim(const mhppo_env *env) { return env ? 20 * env->c.P + 8 * env->c.nC + 4 : MHPPO_EINVAL; }
+int mhppo_env_state_dim(const mhppo_env *env) { return env ? 21 * env->c.P + 8 * env->c.nC + 4 : MHPPO_EINVAL; }
 
 int mhppo_env_reset(mhppo_env *env, float *obs, void *stream) {
   if (!env) return set_error(MHPPO_EINVAL, "null env");

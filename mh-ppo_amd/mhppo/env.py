@@ -105,7 +105,7 @@ class VecCrosswalk:
         return obs, rew, rl, done.bool()
 
     def get_state(self):
-        """[N, state_dim] float64: per ped 20, per car slot 8, then cross, time, ped_traffic, car_traffic."""
+        """[N, state_dim] float64: per ped 20, per car slot 8, cross, time, ped_traffic, car_traffic, ped exist."""
         out = self._t((self.n_envs, self.state_dim), torch.float64)
         _lib.check(_lib.lib().mhppo_env_get_state(self._h, _lib.ptr(out), _lib.stream_ptr()))
         return out

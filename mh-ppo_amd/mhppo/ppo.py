@@ -51,50 +51,61 @@ def global_count(n, device):
     return float(_allreduce_(t).item())
 
 
-def normalized_advantage(ret, value, m_global):
-    L = _lib.lib()
-    st = _lib.stream_ptr()
+# ---------------------------------------------------------------- kernel layer
+# Thin wrappers over the HIP entry points (include/mhppo.h).  Each returns this
+# rank's LOCAL contribution; the DP orchestration below decides what is reduced.
+
+def k_adv_stats(ret, value):
+    """(sum A, sum A^2) over local rows, float64 [2]."""
     stats = torch.zeros(2, dtype=torch.float64, device=ret.device)
-    M = ret.numel()
     v = value.detach().contiguous()
-    _lib.check(L.mhppo_adv_stats(_lib.ptr(ret), _lib.ptr(v), M, _lib.ptr(stats), st))
-    _allreduce_(stats)
+    _lib.check(_lib.lib().mhppo_adv_stats(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
+                                          _lib.stream_ptr()))
+    return stats
+
+
+def k_adv_normalize(ret, value, stats, m_global):
     adv = torch.empty_like(ret)
-    _lib.check(L.mhppo_adv_normalize(_lib.ptr(ret), _lib.ptr(v), M, _lib.ptr(stats), float(m_global),
-                                     _lib.ptr(adv), st))
+    v = value.detach().contiguous()
+    _lib.check(_lib.lib().mhppo_adv_normalize(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
+                                              float(m_global), _lib.ptr(adv), _lib.stream_ptr()))
     return adv
 
 
-def mse_grad(value, ret, m_global):
-    L = _lib.lib()
+def k_mse(value, ret, m_global):
     dv = torch.empty_like(ret)
     loss = torch.zeros(1, dtype=torch.float64, device=ret.device)
     v = value.detach().contiguous()
-    _lib.check(L.mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global, _lib.ptr(dv),
-                                   _lib.ptr(loss), _lib.stream_ptr()))
+    _lib.check(_lib.lib().mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global, _lib.ptr(dv),
+                                            _lib.ptr(loss), _lib.stream_ptr()))
     return dv, loss
 
 
-def ppo_cont_grad(mu, act, logp_old, adv, m_global):
-    L = _lib.lib()
+def k_ppo_cont(mu, act, logp_old, adv, m_global):
     dmu = torch.empty_like(adv)
     loss = torch.zeros(1, dtype=torch.float64, device=adv.device)
     m = mu.detach().contiguous()
-    _lib.check(L.mhppo_ppo_cont_fwd_bwd(_lib.ptr(m), _lib.ptr(act), _lib.ptr(logp_old), _lib.ptr(adv),
-                                        adv.numel(), 1.0 / m_global, _lib.ptr(dmu), _lib.ptr(loss),
-                                        _lib.stream_ptr()))
+    _lib.check(_lib.lib().mhppo_ppo_cont_fwd_bwd(_lib.ptr(m), _lib.ptr(act), _lib.ptr(logp_old), _lib.ptr(adv),
+                                                 adv.numel(), 1.0 / m_global, _lib.ptr(dmu), _lib.ptr(loss),
+                                                 _lib.stream_ptr()))
     return dmu, loss
 
 
-def ppo_choice_grad(probs, logp_old, adv, counts, m_global):
-    L = _lib.lib()
+def k_ppo_choice(probs, logp_old, adv, counts, m_global):
     p = probs.detach().contiguous()
     dp = torch.empty_like(p)
     loss = torch.zeros(1, dtype=torch.float64, device=adv.device)
-    _lib.check(L.mhppo_ppo_choice_fwd_bwd(_lib.ptr(p), _lib.ptr(logp_old), _lib.ptr(adv), adv.numel(),
-                                          _lib.ptr(counts), 1.0 / (m_global * m_global), _lib.ptr(dp),
-                                          _lib.ptr(loss), _lib.stream_ptr()))
+    _lib.check(_lib.lib().mhppo_ppo_choice_fwd_bwd(_lib.ptr(p), _lib.ptr(logp_old), _lib.ptr(adv), adv.numel(),
+                                                   _lib.ptr(counts), 1.0 / (m_global * m_global), _lib.ptr(dp),
+                                                   _lib.ptr(loss), _lib.stream_ptr()))
     return dp, loss
+
+
+# ------------------------------------------------------------- DP orchestration
+
+def normalized_advantage(ret, value, m_global):
+    stats = _allreduce_(k_adv_stats(ret, value))
+    return k_adv_normalize(ret, value, stats, m_global)
 
 
 def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
@@ -102,15 +113,15 @@ def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
     V = torch.squeeze(critic(obs), -1)
     adv = normalized_advantage(ret, V, m_global)
     mu = torch.squeeze(actor(obs), -1)
-    dmu, la = ppo_cont_grad(mu, act, logp_old, adv, m_global)
-    dv, lc = mse_grad(V, ret, m_global)
+    dmu, la = k_ppo_cont(mu, act, logp_old, adv, m_global)
+    dv, lc = k_mse(V, ret, m_global)
     opt_actor.zero_grad(set_to_none=False)
     opt_critic.zero_grad(set_to_none=False)
     torch.autograd.backward([mu, V], [dmu, dv])
     _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
     opt_actor.step()
     opt_critic.step()
-    return la, lc
+    return la, lc  # this rank's loss sums (logging only; reduce if needed)
 
 
 def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts):
@@ -118,12 +129,12 @@ def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
     V = torch.squeeze(critic(obs), -1)
     adv = normalized_advantage(ret, V, m_global)
     probs = actor(obs).reshape(-1, 2)
-    dp, la = ppo_choice_grad(probs, logp_old, adv, counts, m_global)
-    dv, lc = mse_grad(V, ret, m_global)
+    dp, la = k_ppo_choice(probs, logp_old, adv, counts, m_global)
+    dv, lc = k_mse(V, ret, m_global)
     opt_actor.zero_grad(set_to_none=False)
     opt_critic.zero_grad(set_to_none=False)
     torch.autograd.backward([probs, V], [dp, dv])
     _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
     opt_actor.step()
     opt_critic.step()
-    return la, lc
+    return la, lc  # this rank's loss sums (logging only; reduce if needed)

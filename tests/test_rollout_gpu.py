@@ -84,3 +84,23 @@ def test_gpu_rollout_matches_oracle_philox(case):
     # inside the 1e-4 bound
     np.testing.assert_allclose(go["rew"], o["rew"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(go["ep_min"], o["ep_min"], rtol=1e-5, atol=1e-5)
+
+
+def test_rollout_is_shard_invariant():
+    """Envs split over two handles (as over two ranks: env_id_offset) replay exactly the
+    single-handle trajectories: per-env CPython streams + global-id Philox counters."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    torch.manual_seed(9)
+    ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+    aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+    full = RolloutGPU(VecCrosswalk("4cars", 128, 4, 1, 2, seed_base=5))
+    ad = Model_PPO(full.dc, 2, 2).cuda()
+    a = _gpu_out(full.collect(ac, aw, ad, seed=1, iteration=2))
+    parts = []
+    for off in (0, 64):
+        ro = RolloutGPU(VecCrosswalk("4cars", 64, 4, 1, 2, seed_base=5, env_id_offset=off))
+        parts.append(_gpu_out(ro.collect(ac, aw, ad, seed=1, iteration=2)))
+    for k in a:
+        assert np.array_equal(a[k], np.concatenate([parts[0][k], parts[1][k]])), k

@@ -31,7 +31,7 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   return h;
 }
 int hs_obs_dim(HostEnv *h) { return h->c.obs_dim; }
-int hs_state_dim(HostEnv *h) { return 20 * h->c.P + 8 * h->c.nC + 4; }
+int hs_state_dim(HostEnv *h) { return 21 * h->c.P + 8 * h->c.nC + 4; }
 void hs_reset(HostEnv *h, float *obs) {
   for (int e = 0; e < h->c.N; e++) {
     switch (h->c.variant) {
