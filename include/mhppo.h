@@ -160,6 +160,19 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
                              int64_t M, const double *counts, double inv_m2, float *dprobs,
                              double *loss, void *stream);
 
+/* Fused continuous-head training pass on f32 MFMA (13 -> 32 -> 64 -> 32 -> 1 Model_PPO):
+ * forward + loss gradient + backward + weight gradient over M rows, replacing the torch
+ * GEMMs/autograd of one train_model_c epoch (:778-815).
+ * kind 0 = critic pass: writes value[M], grad = dMSE/dW (packed torch layout, 4673 floats),
+ *          sums[0..2] += (sum (V-G)^2, sum A, sum A^2) with A = G - V.
+ * kind 1 = actor pass: reads value[M] and the GLOBAL (sum A, sum A^2) in stats[0..1];
+ *          grad = dL_clip/dW, sums[0] += sum of clip-surrogate terms.
+ * out_mean/out_std: the actor's tanh affine (mean, std); 1/M_global scaling applied. */
+int mhppo_mlp_train_cont(int kind, const float *packed, const float *X, int64_t M, const float *ret,
+                         float *value, const float *act, const float *logp_old, const double *stats,
+                         double m_global, float out_mean, float out_std, float *grad, double *sums,
+                         void *stream);
+
 /* Critic MSE (:808-809): loss += sum (V-G)^2, dV = 2 (V-G) * inv_m. */
 int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv,
                       double *loss, void *stream);

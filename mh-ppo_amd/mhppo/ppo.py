@@ -101,6 +101,31 @@ def k_ppo_choice(probs, logp_old, adv, counts, m_global):
     return dp, loss
 
 
+N_PARAMS_CONT = 13 * 32 + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 + 1  # 4673
+
+
+def k_mlp_train_cont(kind, net, obs, ret, value, act, logp_old, stats, m_global):
+    """Fused forward/loss/backward of a continuous-head net (mhppo_mlp_train_cont).
+    kind 0 (critic): returns (grad[4673], sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
+    kind 1 (actor):  returns (grad[4673], sums[3] = (sum clip-surrogate, 0, 0), None)."""
+    if net.n_in != 13 or net.n_out != 1 or (kind == 0) != (net.model_type == 0):
+        raise ValueError("fused continuous-head kernel needs a 13->1 Model_PPO of the matching kind")
+    dev = obs.device
+    M = obs.shape[0]
+    V = torch.empty(M, dtype=torch.float32, device=dev) if kind == 0 else value.detach().contiguous()
+    grad = torch.empty(N_PARAMS_CONT, dtype=torch.float32, device=dev)
+    sums = torch.zeros(3, dtype=torch.float64, device=dev)
+    obs, ret = obs.float().contiguous(), ret.float().contiguous()
+    act = None if act is None else act.float().contiguous()
+    logp_old = None if logp_old is None else logp_old.float().contiguous()
+    w = net.packed()
+    p = _lib.ptr
+    _lib.check(_lib.lib().mhppo_mlp_train_cont(
+        kind, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), float(m_global),
+        float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
+    return grad, sums, (V if kind == 0 else None)
+
+
 # ------------------------------------------------------------- DP orchestration
 
 def normalized_advantage(ret, value, m_global):
@@ -108,8 +133,38 @@ def normalized_advantage(ret, value, m_global):
     return k_adv_normalize(ret, value, stats, m_global)
 
 
+def _set_grads(net, flat):
+    off = 0
+    for lay in (net.layer1, net.layer2, net.layer3, net.layer4):
+        for p in (lay.weight, lay.bias):
+            n = p.numel()
+            g = flat[off:off + n].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            off += n
+
+
 def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
-    """One full-batch epoch of Algo_PPO.train_model_c (:778-815). Returns (actor_loss, critic_loss)."""
+    """One full-batch epoch of Algo_PPO.train_model_c (:778-815) on the fused MFMA kernel:
+    critic pass (V, MSE gradient, advantage sums) -> all-reduce of the sums -> actor pass
+    (clip-surrogate gradient w.r.t. the start-of-epoch critic's advantage) -> one gradient
+    all-reduce -> Adam.  Returns this rank's (actor, critic) loss sums (float64 tensors)."""
+    gc, sc, V = k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, m_global)
+    stats = _allreduce_(sc[1:3].clone())
+    ga, sa, _ = k_mlp_train_cont(1, actor, obs, ret, V, act, logp_old, stats, m_global)
+    _set_grads(critic, gc)
+    _set_grads(actor, ga)
+    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+    opt_actor.step()
+    opt_critic.step()
+    return sa[0:1], sc[0:1]
+
+
+def train_model_c_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
+    """train_model_c with the MLPs in PyTorch autograd and the PPO arithmetic in HIP
+    (kept as the cross-check for the fused kernel)."""
     V = torch.squeeze(critic(obs), -1)
     adv = normalized_advantage(ret, V, m_global)
     mu = torch.squeeze(actor(obs), -1)

@@ -49,7 +49,22 @@ def _install_cpu_doubles(ppo):
         dmu = (1.0 / m) * (-g) * r * x.double() / L
         return dmu.float(), (-torch.minimum(s1, s2)).sum().reshape(1)
 
+    def mlp_train_cont(kind, net, obs, ret, value, act, lp_old, stats, m):
+        params = list(net.parameters())
+        out = torch.squeeze(net(obs), -1)
+        if kind == 0:
+            dv, loss = mse(out, ret, m)
+            st = adv_stats(ret, out)
+            sums = torch.cat([loss, st])
+            g = torch.autograd.grad(out, params, dv)
+            return torch.cat([x.reshape(-1) for x in g]), sums, out.detach()
+        adv = adv_normalize(ret, value, stats, m)
+        dmu, loss = ppo_cont(out, act, lp_old, adv, m)
+        g = torch.autograd.grad(out, params, dmu)
+        return torch.cat([x.reshape(-1) for x in g]), torch.cat([loss, torch.zeros(2, dtype=torch.float64)]), None
+
     ppo.k_adv_stats, ppo.k_adv_normalize, ppo.k_mse, ppo.k_ppo_cont = adv_stats, adv_normalize, mse, ppo_cont
+    ppo.k_mlp_train_cont = mlp_train_cont
 
 
 def _run(rank, world, port, data, out_q):

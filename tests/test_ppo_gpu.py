@@ -78,3 +78,37 @@ def test_philox_noise_moments():
     y = torch.empty(1000, device="cuda")
     _lib.check(_lib.lib().mhppo_philox_normal(7, 5000, _lib.ptr(y), 1000, _lib.stream_ptr()))
     assert torch.equal(y, x[5000:6000])
+
+
+@pytest.mark.parametrize("M", [1, 31, 33, 1000, 70001])
+def test_fused_cont_grads_vs_autograd(M):
+    """mhppo_mlp_train_cont (fused MFMA forward/backward) vs torch autograd of the same
+    losses on the same weights: V bit-close, loss sums 1e-5 rel, gradients within 1e-4 of
+    the gradient's max-abs (fp32 accumulation order differs)."""
+    from mhppo import ppo
+    from mhppo.models import Model_PPO
+    torch.manual_seed(M)
+    actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+    critic = Model_PPO(13, 1, 0).cuda()
+    obs = (torch.randn(M, 13) * 3).cuda()
+    ret = (torch.randn(M) * 8 - 20).cuda()
+    act = (torch.randn(M) - 1).cuda()
+    lp = (torch.randn(M) * 0.3 - 0.9).cuda()
+    m = float(M) if M > 1 else 2.0  # unbiased std needs m > 1
+    gc, sc, V = ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, m)
+    Vt = torch.squeeze(critic(obs), -1)
+    torch.testing.assert_close(V, Vt.detach(), rtol=1e-5, atol=1e-5)
+    dv, lc = ppo.k_mse(Vt, ret, m)
+    st = ppo.k_adv_stats(ret, Vt)
+    gct = torch.cat([g.reshape(-1) for g in torch.autograd.grad(Vt, list(critic.parameters()), dv)])
+    assert abs(float(sc[0]) - float(lc[0])) <= 1e-5 * abs(float(lc[0])) + 1e-6
+    torch.testing.assert_close(sc[1:3], st, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(gc, gct, rtol=0, atol=1e-4 * float(gct.abs().max()) + 1e-9)
+    stats = st
+    ga, sa, _ = ppo.k_mlp_train_cont(1, actor, obs, ret, Vt, act, lp, stats, m)
+    mu = torch.squeeze(actor(obs), -1)
+    adv = ppo.k_adv_normalize(ret, Vt, stats, m)
+    dmu, la = ppo.k_ppo_cont(mu, act, lp, adv, m)
+    gat = torch.cat([g.reshape(-1) for g in torch.autograd.grad(mu, list(actor.parameters()), dmu)])
+    assert abs(float(sa[0]) - float(la[0])) <= 1e-5 * abs(float(la[0])) + 1e-6
+    torch.testing.assert_close(ga, gat, rtol=0, atol=1e-4 * float(gat.abs().max()) + 1e-9)
