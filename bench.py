@@ -11,10 +11,13 @@ Workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
 value = (all ranks' envs) * 80 env-steps / max-over-ranks iteration time.
 
 Extra JSON fields:
-  roofline     — the fused sample+env-step kernel (mhppo_rollout_sample_env):
-                 algorithmic bytes per env-step x N / its mean
-                 duration, from HIP events recorded on its stream inside the
-                 timed region; peak 8 TB/s HBM.
+  roofline     — the dominant kernel, the fused continuous-head train kernel
+                 (mhppo_mlp_train_cont, ~60 % of GPU time): algorithmic FLOPs per
+                 row x rows / launch duration, from HIP events on
+                 its stream inside the timed region, summed over all launches;
+                 f32 MFMA peak 157.3 TFLOP/s (exact-f32 matrix rate on gfx950).
+  roofline_env — the fused sample+env-step kernel (mhppo_rollout_sample_env):
+                 algorithmic bytes per env-step x N / its mean duration; 8 TB/s.
   cpu_baseline — the C oracle (same env + rollout, glibc) + PyTorch-CPU update
                  on a bounded sample of the same workload, rank 0, N=1 only.
 """
@@ -32,6 +35,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec at 65536 envs × 4 agents, 1/2/4/8 MI355X + %HBM roofline"
 HBM_PEAK_GBS = 8000.0
+F32_MFMA_PEAK_TFLOPS = 157.3
 
 
 def env_step_bytes(S, nC, P, obs_dim, T=80):
@@ -92,6 +96,7 @@ def main():
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
+    from mhppo import ppo
 
     N, T = a.envs, 80
     venv = VecCrosswalk(a.variant, N, a.nb_car, a.nb_ped, a.nb_lines, seed_base=0, env_id_offset=rank * N,
@@ -117,6 +122,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ppo.TRAIN_EVENTS = []
     t0 = time.perf_counter()
     for k in range(a.steps):
         iteration(events[k])
@@ -135,7 +141,14 @@ def main():
     nC = 2 * S if a.variant == "4cars" else S
     per_env = env_step_bytes(S, nC, a.nb_ped, venv.obs_dim)
     achieved = per_env * N / (kern_ms * 1e-3) / 1e9
+    tr = ppo.TRAIN_EVENTS
+    ppo.TRAIN_EVENTS = None
+    tr_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in tr)
+    tr_rows = sum(m for _, m, _, _ in tr)
+    tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
+    tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic = os.environ.get("MHPPO_PMC_BYTES_PER_LAUNCH")
+    traffic_env = os.environ.get("MHPPO_PMC_BYTES_PER_ENV_LAUNCH")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -144,10 +157,15 @@ def main():
         "config": {"workload": f"{a.variant} nb_car={a.nb_car} nb_ped={a.nb_ped} nb_lines={a.nb_lines}, "
                                f"{N} envs/GPU x 80 steps, full PPO iteration (rollout + returns + 10+10 epochs)",
                    "envs_per_gpu": N, "agents": S, "T": T, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": float(traffic) if traffic else None, "bytes_per_env_step": per_env,
-                     "kernel_ms": kern_ms},
+        "roofline": {"bound": "mfma", "kernel": "k_mlp_train (fused continuous-head fwd/loss/bwd/wgrad, f32 MFMA)",
+                     "achieved": tr_tflops, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tr_tflops / F32_MFMA_PEAK_TFLOPS, "traffic": float(traffic) if traffic else None,
+                     "flops_per_row": ppo.FLOPS_PER_ROW_CONT, "rows_per_launch": tr_rows / max(len(tr), 1),
+                     "launches": len(tr), "launch_ms": tr_ms / max(len(tr), 1)},
+        "roofline_env": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": float(traffic_env) if traffic_env else None, "bytes_per_env_step": per_env,
+                         "kernel_ms": kern_ms},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a)

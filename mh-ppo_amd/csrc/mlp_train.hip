@@ -24,7 +24,7 @@
 //   (std_A + 1e-10) from the global statistics; PPO clip surrogate with float64
 //   ratio (:795-806); dy = dL/dmu * std * (1 - tanh^2).
 // Outputs per wave: the packed torch-layout gradient (4673 floats) and float64
-// partial sums; mhppo_mlp_grad_reduce sums the per-wave partials in fixed order.
+// partial sums; k_grad_stage1/2 sum the per-wave partials in fixed order.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -315,25 +315,43 @@ __global__ void __launch_bounds__(64 * WAVES)
   }
 }
 
-// grad[k] = sum_w gpart[w][k] (float64, fixed order); out3 += sum_w dpart[w][0..2]
+// Deterministic two-stage gradient reduction over the per-wave partials (fixed order,
+// float64): stage 1 sums contiguous groups of waves, stage 2 sums the RG group totals.
+constexpr int RG = 32;
+constexpr int NWD = NW + 3;  // gradient + (loss, sum A, sum A^2)
+
 __global__ void __launch_bounds__(256)
-    k_grad_reduce(const float *gpart, int nw, float *grad, const double *dpart, double *out3) {
+    k_grad_stage1(const float *gpart, const double *dpart, int nw, double *tmp) {
   int k = blockIdx.x * 256 + threadIdx.x;
+  int g = blockIdx.y;
+  int i0 = (int)((int64_t)g * nw / RG), i1 = (int)((int64_t)(g + 1) * nw / RG);
+  double s = 0.0;
   if (k < NW) {
-    double s = 0.0;
-    for (int i = 0; i < nw; i++) s += (double)gpart[(size_t)i * NW + k];
-    grad[k] = (float)s;
+    for (int i = i0; i < i1; i++) s += (double)gpart[(size_t)i * NW + k];
+  } else if (k < NWD) {
+    for (int i = i0; i < i1; i++) s += dpart[(size_t)i * 3 + (k - NW)];
+  } else {
+    return;
   }
-  if (blockIdx.x == 0 && threadIdx.x < 3 && out3) {
-    double s = 0.0;
-    for (int i = 0; i < nw; i++) s += dpart[(size_t)i * 3 + threadIdx.x];
-    out3[threadIdx.x] += s;
-  }
+  tmp[(size_t)g * NWD + k] = s;
 }
 
-struct Work {
+__global__ void __launch_bounds__(256) k_grad_stage2(const double *tmp, float *grad, double *out3) {
+  int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= NWD) return;
+  double s = 0.0;
+#pragma unroll 8
+  for (int g = 0; g < RG; g++) s += tmp[(size_t)g * NWD + k];
+  if (k < NW)
+    grad[k] = (float)s;
+  else if (out3)
+    out3[k - NW] += s;
+}
+
+struct Work {  // per-device partial buffers (calls on one device must share one stream)
   float *g = nullptr;
   double *d = nullptr;
+  double *t = nullptr;
   int nw = 0;
 };
 Work g_work[16];
@@ -363,8 +381,10 @@ extern "C" int mhppo_mlp_train_cont(int kind, const float *packed, const float *
   if (wk.nw < nw) {
     if (wk.g) (void)hipFree(wk.g);
     if (wk.d) (void)hipFree(wk.d);
+    if (wk.t) (void)hipFree(wk.t);
     if (hipMalloc(&wk.g, sizeof(float) * (size_t)nw * NW) != hipSuccess ||
-        hipMalloc(&wk.d, sizeof(double) * (size_t)nw * 3) != hipSuccess) {
+        hipMalloc(&wk.d, sizeof(double) * (size_t)nw * 3) != hipSuccess ||
+        hipMalloc(&wk.t, sizeof(double) * (size_t)RG * NWD) != hipSuccess) {
       wk = Work{};
       return set_error(MHPPO_ENOMEM, "mlp_train partials");
     }
@@ -378,7 +398,8 @@ extern "C" int mhppo_mlp_train_cont(int kind, const float *packed, const float *
   else
     hipLaunchKernelGGL(k_mlp_train<1>, grid, blk, shm, s, packed, X, M, ret, value, act, logp_old, stats, m_global,
                        out_mean, out_std, wk.g, wk.d);
-  hipLaunchKernelGGL(k_grad_reduce, dim3((NW + 255) / 256), dim3(256), 0, s, wk.g, nw, grad, wk.d, sums);
+  hipLaunchKernelGGL(k_grad_stage1, dim3((NWD + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, wk.t);
+  hipLaunchKernelGGL(k_grad_stage2, dim3((NWD + 255) / 256), dim3(256), 0, s, wk.t, grad, sums);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

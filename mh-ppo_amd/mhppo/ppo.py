@@ -101,6 +101,14 @@ def k_ppo_choice(probs, logp_old, adv, counts, m_global):
     return dp, loss
 
 
+# Optional launch timing (bench.py): when a list, each fused train launch appends
+# (kind, rows, start_event, end_event) recorded on the launch stream.
+TRAIN_EVENTS = None
+
+# Algorithmic FLOPs of one row through the fused kernel:
+# forward 2*4544, backward data (no dX) 2*(32 + 2048 + 2048), weight grads 2*4544.
+FLOPS_PER_ROW_CONT = 2 * 4544 + 2 * (32 + 2048 + 2048) + 2 * 4544
+
 N_PARAMS_CONT = 13 * 32 + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 + 1  # 4673
 
 
@@ -120,9 +128,16 @@ def k_mlp_train_cont(kind, net, obs, ret, value, act, logp_old, stats, m_global)
     logp_old = None if logp_old is None else logp_old.float().contiguous()
     w = net.packed()
     p = _lib.ptr
+    ev = None
+    if TRAIN_EVENTS is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     _lib.check(_lib.lib().mhppo_mlp_train_cont(
         kind, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), float(m_global),
         float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
+    if ev is not None:
+        ev[1].record()
+        TRAIN_EVENTS.append((kind, M, ev[0], ev[1]))
     return grad, sums, (V if kind == 0 else None)
 
 
