@@ -37,17 +37,24 @@ using namespace mhppo;
 namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int WAVES = 4;
+constexpr int WAVES = 8;  // one 512-thread block per CU: 2 waves per SIMD (<= 256 registers each)
 constexpr int NIN = 13;
 constexpr int NW = 32 * NIN + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 + 1;  // 4673 packed params
 constexpr int S1 = 15, S2 = 33, S3 = 65, ST = 33;                          // LDS row strides
 // LDS layout (floats)
 constexpr int O_W1 = 0, O_B1 = O_W1 + 32 * S1, O_W2 = O_B1 + 32, O_B2 = O_W2 + 64 * S2, O_W3 = O_B2 + 64,
               O_B3 = O_W3 + 32 * S3, O_W4 = O_B3 + 32, O_B4 = O_W4 + 32, O_WEND = O_B4 + 4;
-constexpr int TILE = 32 * ST;                   // one transposed 32x32 tile
-constexpr int O_X = 0, O_T = 32 * NIN;          // per-wave scratch: X tile, then 3 tiles
-constexpr int WAVE_LDS = O_T + 3 * TILE + 32;   // + dy row
-constexpr int LDS_FLOATS = O_WEND + WAVES * WAVE_LDS;
+constexpr int TILE = 32 * ST;  // one transposed 32x32 tile
+// per-wave input slot (one 32-row tile): X [32][13], s0 = [ret 32 | V 32], s1 = [act 32 | logp_old 32]
+constexpr int IN_X = 0, IN_S0 = 32 * NIN, IN_S1 = IN_S0 + 64, IN_SZ = IN_S1 + 64;
+// per-wave scratch: 3 transpose tiles, then 2 input slots (double buffer filled by LDS-DMA)
+constexpr int O_T = 0, O_IN = 3 * TILE;
+constexpr int WAVE_LDS = O_IN + 2 * IN_SZ;
+constexpr int O_DACC = O_WEND + WAVES * WAVE_LDS;        // float64 [WAVES][3][32] per-lane running sums
+constexpr int LDS_FLOATS = O_DACC + WAVES * 3 * 32 * 2;  // 40420 floats = 161,680 B
+static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+static_assert(O_DACC % 2 == 0, "8-B aligned float64 sums");
+static_assert(O_WEND % 4 == 0 && WAVE_LDS % 4 == 0 && O_IN % 4 == 0, "16-B aligned LDS-DMA slots");
 // packed gradient offsets (torch layout)
 constexpr int G_W1 = 0, G_B1 = 32 * NIN, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
               G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32;
@@ -61,11 +68,80 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// scheduling fence between phases: keeps the scheduler from hoisting the next phase's LDS
+// operand reads (and their registers) into the current one
+__device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
   for (int i = 0; i < 16; i++) z[i] = 0.0f;
   return z;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+// Raw buffer resource over [p, p + bytes): SGPR base, 32-bit VGPR lane offsets (no 64-bit
+// per-lane pointers for the compiler to hoist and spill), hardware range check (loads past
+// `bytes` return 0, stores past it are dropped).  dword3 = gfx9 raw-buffer format.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+// LDS-DMA (buffer_load ... lds): lane l's dword(s) land at lds_base + l * size, lds_base
+// wave-uniform (M0).  Issued from inline asm so the compiler's waitcnt pass does not see
+// it: the pass cannot tell the DMA'd slot from other LDS and would put vmcnt(0) before
+// every LDS read, draining the prefetch; the kernel counts vmcnt itself (wait_vmcnt).
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i rsrc_v(const void *p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  v4i d;
+  d.x = (int)(uint32_t)a;
+  d.y = (int)(uint32_t)(a >> 32) & 0xffff;  // stride 0
+  d.z = (int)bytes;
+  d.w = 0x00020000;
+  return d;
+}
+__device__ __forceinline__ uint32_t lds_addr(const float *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
+}
+__device__ __forceinline__ void dma16(v4i r, const float *lds_base, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds_addr(lds_base))
+      : "memory");
+}
+__device__ __forceinline__ void dma4(v4i r, const float *lds_base, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds_addr(lds_base))
+      : "memory");
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15); the
+// compiler does not track LDS-DMA completion, so reads of a DMA'd slot wait explicitly.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N < 16, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+}
+__device__ __forceinline__ float relu0(float x) { return __builtin_fmaxf(x, 0.0f); }
+// v[r] = relu(v[r] + b[feature(r, l)]): the 4 features of register group q are contiguous
+__device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
+  const float4 *b4 = reinterpret_cast<const float4 *>(b);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    float4 c = b4[2 * q + kh];
+    v[4 * q + 0] = relu0(v[4 * q + 0] + c.x);
+    v[4 * q + 1] = relu0(v[4 * q + 1] + c.y);
+    v[4 * q + 2] = relu0(v[4 * q + 2] + c.z);
+    v[4 * q + 3] = relu0(v[4 * q + 3] + c.w);
+  }
 }
 
 // store a C tile (lane = row j, registers = feature(r,l)) as T[feature][row]
@@ -82,6 +158,37 @@ __device__ __forceinline__ float row_sum(const float *T, int l) {
   return s;
 }
 
+// Inputs of one full 32-row tile -> an input slot, by LDS-DMA (no VGPRs, no wait here).
+// X: 416 contiguous floats = 104 16-B chunks (64 + 40 lanes); s0/s1: one dword per lane,
+// exec masks pick the lanes (a DMA's inactive lanes write nothing).
+template <int KIND>
+__device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const float *ret, const float *V,
+                                              const float *act, const float *lp, int64_t row0, int l) {
+  const v4i rx = rsrc_v(X + row0 * NIN, 32 * NIN * 4);
+  dma16(rx, slot + IN_X, 16 * l);
+  if (l < 40) dma16(rx, slot + IN_X + 256, 1024 + 16 * l);
+  const uint32_t vo = 4 * (l & 31);
+  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + IN_S0, vo);
+  if (KIND == 1) {
+    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + IN_S0, vo);
+    if (l < 32) dma4(rsrc_v(act + row0, 128), slot + IN_S1, vo);
+    if (l >= 32) dma4(rsrc_v(lp + row0, 128), slot + IN_S1, vo);
+  }
+}
+template <int KIND>
+constexpr int prefetch_ops() { return KIND == 0 ? 3 : 6; }  // DMA instructions per prefetch
+
+// The ragged last tile (nrows < 32): ordinary buffer loads, rows past M read as 0.
+template <int KIND>
+__device__ __forceinline__ void load_tile_sync(float *slot, const float *X, const float *ret, const float *V,
+                                               const float *act, const float *lp, int64_t row0, int nrows, int l) {
+  const auto rx = rsrc(X + row0 * NIN, (uint32_t)nrows * NIN * 4);
+  for (int q = l; q < 32 * NIN; q += 64) slot[IN_X + q] = bload(rx, 4 * q);
+  const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
+  slot[IN_S0 + l] = bload(rsrc((l < 32 || KIND == 0) ? ret + row0 : V + row0, nb), vo);
+  if (KIND == 1) slot[IN_S1 + l] = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(64 * WAVES)
     k_mlp_train(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
@@ -89,7 +196,8 @@ __global__ void __launch_bounds__(64 * WAVES)
                 const double *__restrict__ stats, double m_global, float out_mean, float out_std,
                 float *__restrict__ gpart, double *__restrict__ dpart) {
   extern __shared__ float lds[];
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile bookkeeping in SGPRs
   // ---- stage weights (padded strides)
   for (int i = tid; i < 32 * NIN; i += 64 * WAVES) lds[O_W1 + (i / NIN) * S1 + i % NIN] = W[i];
   for (int i = tid; i < 32 * S1; i += 64 * WAVES)
@@ -105,7 +213,7 @@ __global__ void __launch_bounds__(64 * WAVES)
   if (tid == 0) lds[O_B4] = W[G_B4];
   __syncthreads();
   float *ws = lds + O_WEND + w * WAVE_LDS;
-  float *Xs = ws + O_X, *T0 = ws + O_T, *T1 = T0 + TILE, *T2 = T1 + TILE, *dys = T2 + TILE;
+  float *T0 = ws + O_T, *T1 = T0 + TILE, *T2 = T1 + TILE;
   const float b4 = lds[O_B4];
   const int j = l & 31;
   const int kh = l >> 5;
@@ -113,7 +221,10 @@ __global__ void __launch_bounds__(64 * WAVES)
   // persistent accumulators
   f32x16 gW1 = zero16(), gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
   float gB1 = 0.f, gB2 = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
-  double acc_loss = 0.0, acc_a = 0.0, acc_a2 = 0.0;
+  // float64 running sums (loss, sum A, sum A^2) live in LDS, one slot per lane of the low
+  // half-wave: keeping them in VGPRs spills, and a spill reload's vmcnt(0) drains the prefetch
+  double *dacc = reinterpret_cast<double *>(lds + O_DACC) + w * 96 + j;
+  if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
   float meanf = 0.f, stdf = 1.f;
   if (KIND == 1) {
     double mean = stats[0] / m_global;
@@ -122,15 +233,26 @@ __global__ void __launch_bounds__(64 * WAVES)
     stdf = (float)sqrt(var > 0 ? var : 0.0);
   }
   const double inv_m = 1.0 / m_global;
-  const int64_t ntiles = (M + 31) / 32;
+  const int64_t ntiles = (M + 31) / 32, nfull = M / 32;
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
 
-  for (int64_t tile = gw; tile < ntiles; tile += nw) {
+  int cb = 0;
+  if (gw < nfull) prefetch_tile<KIND>(ws + O_IN, X, ret, V, act, lp_old, gw * 32, l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
-    // ---- X tile -> LDS [row][13]
-    for (int q = l; q < 32 * NIN; q += 64) Xs[q] = (q / NIN < nrows) ? X[row0 * NIN + q] : 0.0f;
+    float *slot = ws + O_IN + cb * IN_SZ;
+    const int64_t nxt = tile + nw;
+    if (nxt < nfull) {
+      prefetch_tile<KIND>(ws + O_IN + (cb ^ 1) * IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
+      wait_vmcnt<prefetch_ops<KIND>()>();  // this tile's DMA (issued one iteration earlier) has landed
+    } else if (tile < nfull) {
+      wait_vmcnt<0>();
+    } else {
+      load_tile_sync<KIND>(slot, X, ret, V, act, lp_old, row0, nrows, l);
+    }
     wave_sync();
+    const float *Xs = slot + IN_X;
     // ---- forward
     f32x16 h1 = zero16();
 #pragma unroll
@@ -140,8 +262,8 @@ __global__ void __launch_bounds__(64 * WAVES)
       float b = (k < NIN) ? Xs[j * NIN + k] : 0.0f;
       h1 = mfma(a, b, h1);
     }
-#pragma unroll
-    for (int r = 0; r < 16; r++) h1[r] = relu(h1[r] + lds[O_B1 + feat(r, l)]);
+    bias_relu(h1, lds + O_B1, kh);
+    phase();
     f32x16 h2a = zero16(), h2b = zero16();
 #pragma unroll
     for (int s = 0; s < 16; s++) {
@@ -149,54 +271,61 @@ __global__ void __launch_bounds__(64 * WAVES)
       h2a = mfma(lds[O_W2 + j * S2 + k], h1[s], h2a);
       h2b = mfma(lds[O_W2 + (32 + j) * S2 + k], h1[s], h2b);
     }
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      h2a[r] = relu(h2a[r] + lds[O_B2 + feat(r, l)]);
-      h2b[r] = relu(h2b[r] + lds[O_B2 + 32 + feat(r, l)]);
-    }
+    bias_relu(h2a, lds + O_B2, kh);
+    bias_relu(h2b, lds + O_B2 + 32, kh);
+    phase();
     f32x16 h3 = zero16();
 #pragma unroll
     for (int s = 0; s < 16; s++) h3 = mfma(lds[O_W3 + j * S3 + feat(s, l)], h2a[s], h3);
 #pragma unroll
     for (int s = 0; s < 16; s++) h3 = mfma(lds[O_W3 + j * S3 + 32 + feat(s, l)], h2b[s], h3);
+    // h2 leaves the registers: ReLU masks as bits, h2b parked in T2 for dW3b, h2a stays
+    // live only until the dW4/dB3 row sums have freed T0
+    uint32_t m2 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) m2 |= ((h2a[r] > 0.0f) ? 1u : 0u) << r | ((h2b[r] > 0.0f) ? 1u : 0u) << (16 + r);
+    put_tile(T2, h2b, l);
+    bias_relu(h3, lds + O_B3, kh);
     float part = 0.0f;
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      h3[r] = relu(h3[r] + lds[O_B3 + feat(r, l)]);
-      part = fmaf(lds[O_W4 + feat(r, l)], h3[r], part);
+    for (int q = 0; q < 4; q++) {
+      float4 c = reinterpret_cast<const float4 *>(lds + O_W4)[2 * q + kh];
+      part = fmaf(c.x, h3[4 * q], part);
+      part = fmaf(c.y, h3[4 * q + 1], part);
+      part = fmaf(c.z, h3[4 * q + 2], part);
+      part = fmaf(c.w, h3[4 * q + 3], part);
     }
     float y = (part + __shfl_xor(part, 32)) + b4;
     // ---- loss gradient dL/dy for this lane's row
-    const int64_t row = row0 + j;
     const bool valid = j < nrows;
     float dy = 0.0f;
     if (valid) {
-      float rt = ret[row];
+      float rt = slot[IN_S0 + j];
       if (KIND == 0) {
         float v = y;
-        if (kh == 0) V[row] = v;
+        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
         float a = rt - v;
         float d = v - rt;
         if (kh == 0) {
-          acc_a += (double)a;
-          acc_a2 += (double)a * (double)a;
-          acc_loss += (double)d * (double)d;
+          dacc[0] += (double)d * (double)d;
+          dacc[32] += (double)a;
+          dacc[64] += (double)a * (double)a;
         }
         dy = (float)(2.0 * inv_m * (double)d);
       } else {
         float t = tanhf(y);
         float mu = t * out_std + out_mean;
-        float a = rt - V[row];
+        float a = rt - slot[IN_S0 + 32 + j];
         float A = (a - meanf) / (stdf + 1e-10f);
-        float diff = (float)((double)act[row] - (double)mu);
+        float diff = (float)((double)slot[IN_S1 + j] - (double)mu);
         float x = diff * MVN_INV_L;
         float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-        double r = exp((double)lp - (double)lp_old[row]);
+        double r = exp((double)lp - (double)slot[IN_S1 + 32 + j]);
         double Ad = (double)A;
         double rc = r < 0.8 ? 0.8 : (r > 1.2 ? 1.2 : r);
         double s1 = r * Ad, s2 = rc * Ad, in = (r >= 0.8 && r <= 1.2) ? 1.0 : 0.0;
         double g = (s1 < s2) ? Ad : ((s2 < s1) ? in * Ad : 0.5 * Ad + 0.5 * in * Ad);
-        if (kh == 0) acc_loss += -(s1 < s2 ? s1 : s2);
+        if (kh == 0) dacc[0] += -(s1 < s2 ? s1 : s2);
         float dmu = (float)(inv_m * (-g) * r * (double)x * (double)MVN_INV_L);
         dy = (dmu * out_std) * (1.0f - t * t);
       }
@@ -205,27 +334,35 @@ __global__ void __launch_bounds__(64 * WAVES)
     // ---- layer 4 backward: dW4 = rowsum(dy * h3), dH3 = w4 * dy masked
     f32x16 g = zero16();
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      g[r] = dy * h3[r];
-      h3[r] = (h3[r] > 0.0f) ? lds[O_W4 + feat(r, l)] * dy : 0.0f;  // h3 := dH3^T
+    for (int q = 0; q < 4; q++) {
+      float4 c = reinterpret_cast<const float4 *>(lds + O_W4)[2 * q + kh];
+      float cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = 4 * q + i;
+        g[r] = dy * h3[r];
+        h3[r] = (h3[r] > 0.0f) ? cw[i] * dy : 0.0f;  // h3 := dH3^T
+      }
     }
     put_tile(T0, g, l);
     put_tile(T1, h3, l);
-    put_tile(T2, h2a, l);
     wave_sync();
+    phase();
     if (kh == 0) {
       gW4 += row_sum(T0, l);
       gB3 += row_sum(T1, l);
     }
-    // dW3[:, 0:32] += dH3^T . H2a
+    wave_sync();
+    phase();
+    put_tile(T0, h2a, l);
+    wave_sync();
+    phase();
+    // dW3[:, 0:32] += dH3^T . H2a ; dW3[:, 32:64] += dH3^T . H2b
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int k = 2 * s + kh;
-      gW3a = mfma(T1[j * ST + k], T2[j * ST + k], gW3a);
+      gW3a = mfma(T1[j * ST + k], T0[j * ST + k], gW3a);
     }
-    wave_sync();
-    put_tile(T2, h2b, l);
-    wave_sync();
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int k = 2 * s + kh;
@@ -241,14 +378,16 @@ __global__ void __launch_bounds__(64 * WAVES)
     }
 #pragma unroll
     for (int r = 0; r < 16; r++) {
-      d2a[r] = (h2a[r] > 0.0f) ? d2a[r] : 0.0f;
-      d2b[r] = (h2b[r] > 0.0f) ? d2b[r] : 0.0f;
+      d2a[r] = ((m2 >> r) & 1u) ? d2a[r] : 0.0f;
+      d2b[r] = ((m2 >> (16 + r)) & 1u) ? d2b[r] : 0.0f;
     }
     wave_sync();
+    phase();
     put_tile(T0, d2a, l);
     put_tile(T1, d2b, l);
     put_tile(T2, h1, l);
     wave_sync();
+    phase();
     gB2 += row_sum(kh ? T1 : T0, l);
     // dW2 += dH2^T . H1
 #pragma unroll
@@ -267,8 +406,10 @@ __global__ void __launch_bounds__(64 * WAVES)
 #pragma unroll
     for (int r = 0; r < 16; r++) d1[r] = (h1[r] > 0.0f) ? d1[r] : 0.0f;
     wave_sync();
+    phase();
     put_tile(T0, d1, l);
     wave_sync();
+    phase();
     if (kh == 0) gB1 += row_sum(T0, l);
     // dW1 += dH1^T . X
 #pragma unroll
@@ -278,6 +419,7 @@ __global__ void __launch_bounds__(64 * WAVES)
       gW1 = mfma(T0[j * ST + k], b, gW1);
     }
     wave_sync();
+    phase();
   }
   // ---- write this wave's partial gradient (packed torch layout)
   float *gp = gpart + (size_t)gw * NW;
@@ -300,7 +442,8 @@ __global__ void __launch_bounds__(64 * WAVES)
   float b4s = gB4;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) b4s += __shfl_xor(b4s, o);
-  double s0 = acc_loss, s1 = acc_a, s2 = acc_a2;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  if (kh == 0) s0 = dacc[0], s1 = dacc[32], s2 = dacc[64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s0 += __shfl_xor(s0, o);
@@ -358,9 +501,9 @@ Work g_work[16];
 
 int grid_waves() {
   int dev = 0, cus = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return cus * 2 * WAVES;  // 2 blocks of 4 waves per CU
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus * WAVES;  // one block of 8 waves per CU
 }
 }  // namespace
 
@@ -371,9 +514,10 @@ extern "C" int mhppo_mlp_train_cont(int kind, const float *packed, const float *
   if (!packed || !X || !ret || !value || !grad || M < 0 || (kind != 0 && kind != 1))
     return set_error(MHPPO_EINVAL, "bad argument");
   if (kind == 1 && (!act || !logp_old || !stats)) return set_error(MHPPO_EINVAL, "actor pass needs act/logp/stats");
+  if (((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   Work &wk = g_work[dev & 15];
   int nw = grid_waves();
   if (M > 0) nw = (int)min((int64_t)nw, ((M + 31) / 32 + WAVES - 1) / WAVES * WAVES);

@@ -1,0 +1,42 @@
+"""Micro-benchmark of the fused continuous-head train kernel (mhppo_mlp_train_cont):
+both passes at M rows, HIP-event timed on the launch stream; prints TFLOP/s."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
+import torch  # noqa: E402
+
+from mhppo import ppo  # noqa: E402
+from mhppo.models import Model_PPO  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=10485760)
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+M = a.rows
+torch.manual_seed(0)
+actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+critic = Model_PPO(13, 1, 0).cuda()
+obs = torch.randn(M, 13, device="cuda") * 3
+ret = torch.randn(M, device="cuda") * 8 - 20
+act = torch.randn(M, device="cuda") - 1
+lp = torch.randn(M, device="cuda") * 0.3 - 0.9
+for kind in (0, 1, 0, 1):
+    gc, sc, V = ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, float(M))
+    ga, sa, _ = ppo.k_mlp_train_cont(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), float(M))
+torch.cuda.synchronize()
+for kind in (0, 1):
+    ppo.TRAIN_EVENTS = []
+    for _ in range(a.reps):
+        if kind == 0:
+            ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, float(M))
+        else:
+            ppo.k_mlp_train_cont(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), float(M))
+    torch.cuda.synchronize()
+    ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
+    tf = ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12
+    print(f"kind {kind} rows {M}: {ms:.3f} ms  {tf:.1f} TFLOP/s "
+          f"({100 * tf / 157.3:.1f}% of f32 MFMA peak)", flush=True)
+ppo.TRAIN_EVENTS = None
