@@ -141,10 +141,10 @@ def main():
     nC = 2 * S if a.variant == "4cars" else S
     per_env = env_step_bytes(S, nC, a.nb_ped, venv.obs_dim)
     achieved = per_env * N / (kern_ms * 1e-3) / 1e9
-    tr = ppo.TRAIN_EVENTS
+    tr = [e for e in ppo.TRAIN_EVENTS if e[1] == 13]  # the continuous heads' launches
     ppo.TRAIN_EVENTS = None
-    tr_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in tr)
-    tr_rows = sum(m for _, m, _, _ in tr)
+    tr_ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in tr)
+    tr_rows = sum(m for _, _, m, _, _ in tr)
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic = os.environ.get("MHPPO_PMC_BYTES_PER_LAUNCH")

@@ -160,18 +160,24 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
                              int64_t M, const double *counts, double inv_m2, float *dprobs,
                              double *loss, void *stream);
 
-/* Fused continuous-head training pass on f32 MFMA (13 -> 32 -> 64 -> 32 -> 1 Model_PPO):
+/* Fused training pass of one Model_PPO head (n_in -> 32 -> 64 -> 32 -> n_out) on f32 MFMA:
  * forward + loss gradient + backward + weight gradient over M rows, replacing the torch
- * GEMMs/autograd of one train_model_c epoch (:778-815).
- * kind 0 = critic pass: writes value[M], grad = dMSE/dW (packed torch layout, 4673 floats),
+ * GEMMs/autograd of one epoch of train_model_c (:778-815) / train_model_d (:818-851).
+ * kind 0 = critic (n_in <= 32, n_out 1): writes value[M]; grad = dMSE/dW;
  *          sums[0..2] += (sum (V-G)^2, sum A, sum A^2) with A = G - V.
- * kind 1 = actor pass: reads value[M] and the GLOBAL (sum A, sum A^2) in stats[0..1];
- *          grad = dL_clip/dW, sums[0] += sum of clip-surrogate terms.
- * out_mean/out_std: the actor's tanh affine (mean, std); 1/M_global scaling applied. */
-int mhppo_mlp_train_cont(int kind, const float *packed, const float *X, int64_t M, const float *ret,
-                         float *value, const float *act, const float *logp_old, const double *stats,
-                         double m_global, float out_mean, float out_std, float *grad, double *sums,
-                         void *stream);
+ * kind 1 = continuous actor (n_in 13, n_out 1, tanh*out_std + out_mean): reads value[M],
+ *          act, logp_old and the GLOBAL (sum A, sum A^2) in stats[0..1];
+ *          grad = d(clip surrogate)/dW, sums[0] += sum of surrogate terms.
+ * kind 2 = choice actor (n_in <= 32, n_out 2, pairwise softmax): reads value, logp_old,
+ *          stats and the GLOBAL action counts counts[0..1] (float64);
+ *          grad = d(O(M) Categorical surrogate / M_global^2)/dW, sums[0] += its sum.
+ * grad: packed torch layout W1 b1 W2 b2 W3 b3 W4 b4 (32 n_in + 4224 + 33 n_out floats).
+ * m_global = the global row count (data parallel: all ranks' rows).
+ * Per-device workspace: calls on one device must be ordered on one stream. */
+int mhppo_mlp_train(int kind, int n_in, const float *packed, const float *X, int64_t M, const float *ret,
+                    float *value, const float *act, const float *logp_old, const double *stats,
+                    const double *counts, double m_global, float out_mean, float out_std, float *grad,
+                    double *sums, void *stream);
 
 /* Critic MSE (:808-809): loss += sum (V-G)^2, dV = 2 (V-G) * inv_m. */
 int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv,

@@ -1,32 +1,40 @@
-// mlp_train.hip — fused forward + loss gradient + backward + weight gradient of
-// one continuous-head Model_PPO (13 -> 32 -> 64 -> 32 -> 1, ReLU;
-// Coop-MH-PPO-scalable.py:42-93) over M rows, on f32 MFMA (v_mfma_f32_32x32x2_f32,
-// exact fp32 products/sums).  Replaces, per epoch and head, the torch forward
-// GEMMs, autograd backward and weight-gradient GEMMs of train_model_c
-// (:778-815) whose K = M reductions ran at ~15 % of HBM bandwidth.
+// mlp_train.hip — fused forward + loss gradient + backward + weight gradient of one
+// Model_PPO head (n_in -> 32 -> 64 -> 32 -> n_out, ReLU; Coop-MH-PPO-scalable.py:42-93)
+// over M rows, on f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 products/sums).
+// Replaces, per epoch and head, the torch forward GEMMs, autograd backward and the
+// K = M weight-gradient GEMMs of train_model_c / train_model_d (:778-851).
 //
-// Geometry: one wave owns a 32-row tile at a time (grid-stride over tiles) and
-// keeps its running weight gradient in registers; 4 waves per block share the
-// weights staged in LDS (padded strides, conflict-free operand reads).
-// Orientation: activations are held TRANSPOSED, H^T [features x 32 rows]: the
-// MFMA C tile then has the row on the lane (l & 31) and the features in the 16
-// registers (feature(r, l) = (r&3) + 8(r>>2) + 4(l>>5)), so register s of a
-// layer's output is the B operand of k-step s of the next layer (k order
-// feature(s, l), matched by the A-operand weight reads) — no data movement
-// between layers, forward or backward.  Weight gradients sum over rows, i.e.
-// need rows on the K axis: the delta and activation tiles go through a
-// wave-local LDS transpose [feature][row] (stride 33) for those MFMAs; bias
-// gradients are row sums of the same LDS tiles.
+// Geometry: one wave owns a 32-row tile at a time (grid-stride over tiles) and keeps
+// its running weight gradient in registers; the waves of a block share the weights
+// staged in LDS (padded strides, conflict-free operand reads).
+// Orientation: activations are held TRANSPOSED, H^T [features x 32 rows]: the MFMA C
+// tile has the row on the lane (l & 31) and the features in the 16 registers
+// (feature(r, l) = (r&3) + 8(r>>2) + 4(l>>5)), so register s of a layer's output is the
+// B operand of k-step s of the next layer (k order feature(s, l), matched by the
+// A-operand weight reads) — no data movement between layers, forward or backward.
+// Weight gradients sum over rows, i.e. need rows on the K axis: the delta and
+// activation tiles go through a wave-local LDS transpose [feature][row] (stride 33) for
+// those MFMAs; bias gradients are row sums of the same LDS tiles.
 //
-// KIND 0 (critic pass): V = net(x); writes V, accumulates (sum A, sum A^2) of
-//   A = ret - V (advantage statistics, :786-787) and the MSE loss; dV = 2(V-ret)/M.
-// KIND 1 (actor pass): mu = tanh(y)*std + mean; A = ((ret - V) - mean_A) /
-//   (std_A + 1e-10) from the global statistics; PPO clip surrogate with float64
-//   ratio (:795-806); dy = dL/dmu * std * (1 - tanh^2).
-// Outputs per wave: the packed torch-layout gradient (4673 floats) and float64
-// partial sums; k_grad_stage1/2 sum the per-wave partials in fixed order.
+// Kinds (the loss the head is trained on):
+//   K_CRITIC  V = net(x); writes V, accumulates (sum A, sum A^2) of A = G - V (the
+//             advantage statistics, :786-787 / :825-826) and the MSE loss; dV = 2(V-G)/M.
+//   K_CONT    continuous actor: mu = tanh(y)*std + mean; A normalised from the GLOBAL
+//             statistics; MVN log-prob, float64 ratio, clip surrogate (:795-806);
+//             dy = dL/dmu * std * (1 - tanh^2).
+//   K_CHOICE  choice actor: p = softmax(y0, y1); the reference's M x M Categorical
+//             broadcast (:828-842) in its exact O(M) form: each row contributes
+//             sum_k counts[k] * f(r_k, A) with r_k = p_k / exp(logp_old); dL/dp through the
+//             pn = p / sum(p) normalisation and the clamp, then the softmax Jacobian.
+// Continuous heads (13 inputs, the big batches) run 8 waves per CU (2 per SIMD) with the
+// next tile's inputs prefetched into a double-buffered LDS slot by LDS-DMA; the other
+// instantiations (choice obs of 12..32 features, small batches) load synchronously.
+// Outputs per wave: the packed torch-layout gradient and float64 partial sums;
+// k_grad_stage1/2 sum the per-wave partials in fixed order (deterministic).
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <algorithm>
 
 #include "../../include/mhppo.h"
 #include "common.h"
@@ -37,27 +45,36 @@ using namespace mhppo;
 namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int WAVES = 8;  // one 512-thread block per CU: 2 waves per SIMD (<= 256 registers each)
-constexpr int NIN = 13;
-constexpr int NW = 32 * NIN + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 + 1;  // 4673 packed params
-constexpr int S1 = 15, S2 = 33, S3 = 65, ST = 33;                          // LDS row strides
-// LDS layout (floats)
-constexpr int O_W1 = 0, O_B1 = O_W1 + 32 * S1, O_W2 = O_B1 + 32, O_B2 = O_W2 + 64 * S2, O_W3 = O_B2 + 64,
-              O_B3 = O_W3 + 32 * S3, O_W4 = O_B3 + 32, O_B4 = O_W4 + 32, O_WEND = O_B4 + 4;
-constexpr int TILE = 32 * ST;  // one transposed 32x32 tile
-// per-wave input slot (one 32-row tile): X [32][13], s0 = [ret 32 | V 32], s1 = [act 32 | logp_old 32]
-constexpr int IN_X = 0, IN_S0 = 32 * NIN, IN_S1 = IN_S0 + 64, IN_SZ = IN_S1 + 64;
-// per-wave scratch: 3 transpose tiles, then 2 input slots (double buffer filled by LDS-DMA)
-constexpr int O_T = 0, O_IN = 3 * TILE;
-constexpr int WAVE_LDS = O_IN + 2 * IN_SZ;
-constexpr int O_DACC = O_WEND + WAVES * WAVE_LDS;        // float64 [WAVES][3][32] per-lane running sums
-constexpr int LDS_FLOATS = O_DACC + WAVES * 3 * 32 * 2;  // 40420 floats = 161,680 B
-static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
-static_assert(O_DACC % 2 == 0, "8-B aligned float64 sums");
-static_assert(O_WEND % 4 == 0 && WAVE_LDS % 4 == 0 && O_IN % 4 == 0, "16-B aligned LDS-DMA slots");
-// packed gradient offsets (torch layout)
-constexpr int G_W1 = 0, G_B1 = 32 * NIN, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
-              G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32;
+enum { K_CRITIC = 0, K_CONT = 1, K_CHOICE = 2 };
+constexpr int NIN_CONT = 13;
+constexpr int S2 = 33, S3 = 65, ST = 33;  // LDS row strides (W2, W3, transpose tiles)
+constexpr int TILE = 32 * ST;             // one transposed 32x32 tile
+
+__host__ __device__ constexpr int n_params(int nin, int nout) {
+  return 32 * nin + 32 + 64 * 32 + 64 + 32 * 64 + 32 + nout * 32 + nout;
+}
+constexpr int NW_MAX = n_params(32, 2);
+
+// LDS layout (floats) of one instantiation: KS = layer-1 k-steps (inputs padded to 2 KS),
+// PF = double-buffered DMA prefetch (13-input heads), NOUT = output width.
+template <int KS, bool PF, int NOUT>
+struct Lay {
+  static constexpr int WAVES = PF ? 8 : 4;  // PF: 2 waves/SIMD (<= 256 VGPRs); else 1
+  static constexpr int S1 = 2 * KS + 1;     // odd W1 row stride
+  static constexpr int O_W1 = 0, O_B1 = 32 * S1, O_W2 = O_B1 + 32, O_B2 = O_W2 + 64 * S2, O_W3 = O_B2 + 64,
+                       O_B3 = O_W3 + 32 * S3, O_W4 = O_B3 + 32, O_B4 = O_W4 + 32 * NOUT,
+                       O_WEND = (O_B4 + NOUT + 3) / 4 * 4;
+  // per-wave input slot: X [32][n_in], s0 = [ret 32 | V 32], s1 = [act or logp_old 32 | logp_old 32]
+  static constexpr int XMAX = PF ? 32 * NIN_CONT : 64 * KS;
+  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = IN_S0 + 64, IN_SZ = IN_S1 + 64;
+  static constexpr int NSLOT = PF ? 2 : 1;
+  // per-wave scratch: 3 transpose tiles, then the input slot(s)
+  static constexpr int O_T = 0, O_IN = 3 * TILE, WAVE_LDS = O_IN + NSLOT * IN_SZ;
+  static constexpr int O_DACC = O_WEND + WAVES * WAVE_LDS;  // float64 [WAVES][3][32]
+  static constexpr int FLOATS = O_DACC + WAVES * 3 * 32 * 2;
+  static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget");
+  static_assert(O_WEND % 4 == 0 && WAVE_LDS % 4 == 0 && O_IN % 4 == 0 && IN_SZ % 4 == 0, "16-B aligned slots");
+};
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -123,8 +140,7 @@ __device__ __forceinline__ void dma4(v4i r, const float *lds_base, uint32_t voff
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
-// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15); the
-// compiler does not track LDS-DMA completion, so reads of a DMA'd slot wait explicitly.
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N < 16, "vmcnt");
@@ -143,7 +159,19 @@ __device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
     v[4 * q + 3] = relu0(v[4 * q + 3] + c.w);
   }
 }
-
+// sum_r w[feature(r, l)] * h[r] over this lane's 16 features
+__device__ __forceinline__ float dot16(const float *w, const f32x16 &h, int kh) {
+  float part = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    float4 c = reinterpret_cast<const float4 *>(w)[2 * q + kh];
+    part = fmaf(c.x, h[4 * q], part);
+    part = fmaf(c.y, h[4 * q + 1], part);
+    part = fmaf(c.z, h[4 * q + 2], part);
+    part = fmaf(c.w, h[4 * q + 3], part);
+  }
+  return part;
+}
 // store a C tile (lane = row j, registers = feature(r,l)) as T[feature][row]
 __device__ __forceinline__ void put_tile(float *T, const f32x16 &v, int l) {
 #pragma unroll
@@ -161,187 +189,237 @@ __device__ __forceinline__ float row_sum(const float *T, int l) {
 // Inputs of one full 32-row tile -> an input slot, by LDS-DMA (no VGPRs, no wait here).
 // X: 416 contiguous floats = 104 16-B chunks (64 + 40 lanes); s0/s1: one dword per lane,
 // exec masks pick the lanes (a DMA's inactive lanes write nothing).
-template <int KIND>
+template <int KIND, class LY>
 __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const float *ret, const float *V,
                                               const float *act, const float *lp, int64_t row0, int l) {
-  const v4i rx = rsrc_v(X + row0 * NIN, 32 * NIN * 4);
-  dma16(rx, slot + IN_X, 16 * l);
-  if (l < 40) dma16(rx, slot + IN_X + 256, 1024 + 16 * l);
+  const v4i rx = rsrc_v(X + row0 * NIN_CONT, 32 * NIN_CONT * 4);
+  dma16(rx, slot + LY::IN_X, 16 * l);
+  if (l < 40) dma16(rx, slot + LY::IN_X + 256, 1024 + 16 * l);
   const uint32_t vo = 4 * (l & 31);
-  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + IN_S0, vo);
-  if (KIND == 1) {
-    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + IN_S0, vo);
-    if (l < 32) dma4(rsrc_v(act + row0, 128), slot + IN_S1, vo);
-    if (l >= 32) dma4(rsrc_v(lp + row0, 128), slot + IN_S1, vo);
+  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + LY::IN_S0, vo);
+  if (KIND == K_CONT) {
+    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + LY::IN_S0, vo);
+    if (l < 32) dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);
+    if (l >= 32) dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1, vo);
   }
 }
 template <int KIND>
-constexpr int prefetch_ops() { return KIND == 0 ? 3 : 6; }  // DMA instructions per prefetch
+constexpr int prefetch_ops() { return KIND == K_CRITIC ? 3 : 6; }  // DMA instructions per prefetch
 
-// The ragged last tile (nrows < 32): ordinary buffer loads, rows past M read as 0.
-template <int KIND>
-__device__ __forceinline__ void load_tile_sync(float *slot, const float *X, const float *ret, const float *V,
-                                               const float *act, const float *lp, int64_t row0, int nrows, int l) {
-  const auto rx = rsrc(X + row0 * NIN, (uint32_t)nrows * NIN * 4);
-  for (int q = l; q < 32 * NIN; q += 64) slot[IN_X + q] = bload(rx, 4 * q);
+// Synchronous tile load (ragged last tile of the DMA path; every tile otherwise):
+// ordinary buffer loads, rows past M read as 0.
+template <int KIND, class LY>
+__device__ __forceinline__ void load_tile_sync(float *slot, const float *X, int nin, const float *ret,
+                                               const float *V, const float *act, const float *lp, int64_t row0,
+                                               int nrows, int l) {
+  const auto rx = rsrc(X + row0 * nin, (uint32_t)(nrows * nin) * 4);
+  for (int q = l; q < 32 * nin; q += 64) slot[LY::IN_X + q] = bload(rx, 4 * q);
   const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
-  slot[IN_S0 + l] = bload(rsrc((l < 32 || KIND == 0) ? ret + row0 : V + row0, nb), vo);
-  if (KIND == 1) slot[IN_S1 + l] = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
+  slot[LY::IN_S0 + l] = bload(rsrc((l < 32 || KIND == K_CRITIC) ? ret + row0 : V + row0, nb), vo);
+  if (KIND == K_CONT) slot[LY::IN_S1 + l] = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
+  if (KIND == K_CHOICE) slot[LY::IN_S1 + l] = bload(rsrc(lp + row0, nb), vo);
 }
 
-template <int KIND>
-__global__ void __launch_bounds__(64 * WAVES)
-    k_mlp_train(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
-                float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
-                const double *__restrict__ stats, double m_global, float out_mean, float out_std,
+template <int KIND, int KS, bool PF>
+__global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
+    k_mlp_train(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
+                const float *__restrict__ ret, float *__restrict__ V, const float *__restrict__ act,
+                const float *__restrict__ lp_old, const double *__restrict__ stats,
+                const double *__restrict__ counts, double m_global, float out_mean, float out_std,
                 float *__restrict__ gpart, double *__restrict__ dpart) {
+  constexpr int NOUT = KIND == K_CHOICE ? 2 : 1;
+  using LY = Lay<KS, PF, NOUT>;
+  constexpr int WAVES = LY::WAVES;
   extern __shared__ float lds[];
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile bookkeeping in SGPRs
-  // ---- stage weights (padded strides)
-  for (int i = tid; i < 32 * NIN; i += 64 * WAVES) lds[O_W1 + (i / NIN) * S1 + i % NIN] = W[i];
-  for (int i = tid; i < 32 * S1; i += 64 * WAVES)
-    if (i % S1 >= NIN) lds[O_W1 + i] = 0.0f;
-  for (int i = tid; i < 32; i += 64 * WAVES) lds[O_B1 + i] = W[G_B1 + i];
-  for (int i = tid; i < 64 * 32; i += 64 * WAVES) lds[O_W2 + (i >> 5) * S2 + (i & 31)] = W[G_W2 + i];
-  for (int i = tid; i < 64; i += 64 * WAVES) lds[O_B2 + i] = W[G_B2 + i];
-  for (int i = tid; i < 32 * 64; i += 64 * WAVES) lds[O_W3 + (i >> 6) * S3 + (i & 63)] = W[G_W3 + i];
-  for (int i = tid; i < 32; i += 64 * WAVES) {
-    lds[O_B3 + i] = W[G_B3 + i];
-    lds[O_W4 + i] = W[G_W4 + i];
+  if (PF) nin = NIN_CONT;
+  // packed torch-layout offsets
+  const int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
+            G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32 * NOUT, NWP = G_B4 + NOUT;
+  // ---- stage weights (padded strides, zero padding)
+  for (int i = tid; i < 32 * LY::S1; i += 64 * WAVES) {
+    const int r = i / LY::S1, c = i % LY::S1;
+    lds[LY::O_W1 + i] = c < nin ? W[G_W1 + r * nin + c] : 0.0f;
   }
-  if (tid == 0) lds[O_B4] = W[G_B4];
+  for (int i = tid; i < 32; i += 64 * WAVES) lds[LY::O_B1 + i] = W[G_B1 + i];
+  for (int i = tid; i < 64 * 32; i += 64 * WAVES) lds[LY::O_W2 + (i >> 5) * S2 + (i & 31)] = W[G_W2 + i];
+  for (int i = tid; i < 64; i += 64 * WAVES) lds[LY::O_B2 + i] = W[G_B2 + i];
+  for (int i = tid; i < 32 * 64; i += 64 * WAVES) lds[LY::O_W3 + (i >> 6) * S3 + (i & 63)] = W[G_W3 + i];
+  for (int i = tid; i < 32; i += 64 * WAVES) lds[LY::O_B3 + i] = W[G_B3 + i];
+  for (int i = tid; i < 32 * NOUT; i += 64 * WAVES) lds[LY::O_W4 + i] = W[G_W4 + i];
+  if (tid < NOUT) lds[LY::O_B4 + tid] = W[G_B4 + tid];
   __syncthreads();
-  float *ws = lds + O_WEND + w * WAVE_LDS;
-  float *T0 = ws + O_T, *T1 = T0 + TILE, *T2 = T1 + TILE;
-  const float b4 = lds[O_B4];
+  float *ws = lds + LY::O_WEND + w * LY::WAVE_LDS;
+  float *T0 = ws + LY::O_T, *T1 = T0 + TILE, *T2 = T1 + TILE;
+  const float b40 = lds[LY::O_B4], b41 = NOUT == 2 ? lds[LY::O_B4 + 1] : 0.0f;
   const int j = l & 31;
   const int kh = l >> 5;
 
   // persistent accumulators
   f32x16 gW1 = zero16(), gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
-  float gB1 = 0.f, gB2 = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
+  float gB1 = 0.f, gB2 = 0.f, gB3 = 0.f, gW40 = 0.f, gW41 = 0.f, gB40 = 0.f, gB41 = 0.f;
   // float64 running sums (loss, sum A, sum A^2) live in LDS, one slot per lane of the low
   // half-wave: keeping them in VGPRs spills, and a spill reload's vmcnt(0) drains the prefetch
-  double *dacc = reinterpret_cast<double *>(lds + O_DACC) + w * 96 + j;
+  double *dacc = reinterpret_cast<double *>(lds + LY::O_DACC) + w * 96 + j;
   if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
   float meanf = 0.f, stdf = 1.f;
-  if (KIND == 1) {
+  if (KIND != K_CRITIC) {
     double mean = stats[0] / m_global;
     double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
     meanf = (float)mean;
     stdf = (float)sqrt(var > 0 ? var : 0.0);
   }
   const double inv_m = 1.0 / m_global;
-  const int64_t ntiles = (M + 31) / 32, nfull = M / 32;
+  const int64_t ntiles = (M + 31) / 32, nfull = PF ? M / 32 : 0;
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
 
   int cb = 0;
-  if (gw < nfull) prefetch_tile<KIND>(ws + O_IN, X, ret, V, act, lp_old, gw * 32, l);
-  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
+  if (PF && gw < nfull) prefetch_tile<KIND, LY>(ws + LY::O_IN, X, ret, V, act, lp_old, gw * 32, l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= (PF ? 1 : 0)) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
-    float *slot = ws + O_IN + cb * IN_SZ;
-    const int64_t nxt = tile + nw;
-    if (nxt < nfull) {
-      prefetch_tile<KIND>(ws + O_IN + (cb ^ 1) * IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
-      wait_vmcnt<prefetch_ops<KIND>()>();  // this tile's DMA (issued one iteration earlier) has landed
-    } else if (tile < nfull) {
-      wait_vmcnt<0>();
+    float *slot = ws + LY::O_IN + cb * LY::IN_SZ;
+    if constexpr (PF) {
+      const int64_t nxt = tile + nw;
+      if (nxt < nfull) {
+        prefetch_tile<KIND, LY>(ws + LY::O_IN + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
+        wait_vmcnt<prefetch_ops<KIND>()>();  // this tile's DMA (issued one iteration earlier) has landed
+      } else if (tile < nfull) {
+        wait_vmcnt<0>();
+      } else {
+        load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
+      }
     } else {
-      load_tile_sync<KIND>(slot, X, ret, V, act, lp_old, row0, nrows, l);
+      load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
     }
     wave_sync();
-    const float *Xs = slot + IN_X;
+    const float *Xs = slot + LY::IN_X;
     // ---- forward
     f32x16 h1 = zero16();
 #pragma unroll
-    for (int s = 0; s < 7; s++) {
+    for (int s = 0; s < KS; s++) {
       int k = 2 * s + kh;
-      float a = lds[O_W1 + j * S1 + k];
-      float b = (k < NIN) ? Xs[j * NIN + k] : 0.0f;
+      float a = lds[LY::O_W1 + j * LY::S1 + k];
+      float b = (k < nin) ? Xs[j * nin + k] : 0.0f;
       h1 = mfma(a, b, h1);
     }
-    bias_relu(h1, lds + O_B1, kh);
+    bias_relu(h1, lds + LY::O_B1, kh);
     phase();
     f32x16 h2a = zero16(), h2b = zero16();
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int k = feat(s, l);
-      h2a = mfma(lds[O_W2 + j * S2 + k], h1[s], h2a);
-      h2b = mfma(lds[O_W2 + (32 + j) * S2 + k], h1[s], h2b);
+      h2a = mfma(lds[LY::O_W2 + j * S2 + k], h1[s], h2a);
+      h2b = mfma(lds[LY::O_W2 + (32 + j) * S2 + k], h1[s], h2b);
     }
-    bias_relu(h2a, lds + O_B2, kh);
-    bias_relu(h2b, lds + O_B2 + 32, kh);
+    bias_relu(h2a, lds + LY::O_B2, kh);
+    bias_relu(h2b, lds + LY::O_B2 + 32, kh);
     phase();
     f32x16 h3 = zero16();
 #pragma unroll
-    for (int s = 0; s < 16; s++) h3 = mfma(lds[O_W3 + j * S3 + feat(s, l)], h2a[s], h3);
+    for (int s = 0; s < 16; s++) h3 = mfma(lds[LY::O_W3 + j * S3 + feat(s, l)], h2a[s], h3);
 #pragma unroll
-    for (int s = 0; s < 16; s++) h3 = mfma(lds[O_W3 + j * S3 + 32 + feat(s, l)], h2b[s], h3);
+    for (int s = 0; s < 16; s++) h3 = mfma(lds[LY::O_W3 + j * S3 + 32 + feat(s, l)], h2b[s], h3);
     // h2 leaves the registers: ReLU masks as bits, h2b parked in T2 for dW3b, h2a stays
     // live only until the dW4/dB3 row sums have freed T0
     uint32_t m2 = 0;
 #pragma unroll
     for (int r = 0; r < 16; r++) m2 |= ((h2a[r] > 0.0f) ? 1u : 0u) << r | ((h2b[r] > 0.0f) ? 1u : 0u) << (16 + r);
     put_tile(T2, h2b, l);
-    bias_relu(h3, lds + O_B3, kh);
-    float part = 0.0f;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      float4 c = reinterpret_cast<const float4 *>(lds + O_W4)[2 * q + kh];
-      part = fmaf(c.x, h3[4 * q], part);
-      part = fmaf(c.y, h3[4 * q + 1], part);
-      part = fmaf(c.z, h3[4 * q + 2], part);
-      part = fmaf(c.w, h3[4 * q + 3], part);
+    bias_relu(h3, lds + LY::O_B3, kh);
+    float part0 = dot16(lds + LY::O_W4, h3, kh);
+    const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
+    float y1 = 0.0f;
+    if constexpr (NOUT == 2) {
+      float part1 = dot16(lds + LY::O_W4 + 32, h3, kh);
+      y1 = (part1 + __shfl_xor(part1, 32)) + b41;
     }
-    float y = (part + __shfl_xor(part, 32)) + b4;
     // ---- loss gradient dL/dy for this lane's row
     const bool valid = j < nrows;
-    float dy = 0.0f;
+    float dy0 = 0.0f, dy1 = 0.0f;
     if (valid) {
-      float rt = slot[IN_S0 + j];
-      if (KIND == 0) {
-        float v = y;
+      const float rt = slot[LY::IN_S0 + j];
+      if constexpr (KIND == K_CRITIC) {
+        const float v = y0;
         if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
-        float a = rt - v;
-        float d = v - rt;
+        const float a = rt - v;
+        const float d = v - rt;
         if (kh == 0) {
           dacc[0] += (double)d * (double)d;
           dacc[32] += (double)a;
           dacc[64] += (double)a * (double)a;
         }
-        dy = (float)(2.0 * inv_m * (double)d);
+        dy0 = (float)(2.0 * inv_m * (double)d);
+      } else if constexpr (KIND == K_CONT) {
+        const float t = tanhf(y0);
+        const float mu = t * out_std + out_mean;
+        const float a = rt - slot[LY::IN_S0 + 32 + j];
+        const float A = (a - meanf) / (stdf + 1e-10f);
+        const float diff = (float)((double)slot[LY::IN_S1 + j] - (double)mu);
+        const float x = diff * MVN_INV_L;
+        const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
+        const double r = exp((double)lp - (double)slot[LY::IN_S1 + 32 + j]);
+        double dfdr;
+        const double f = surr_and_grad(r, (double)A, dfdr);
+        if (kh == 0) dacc[0] += f;
+        const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+        dy0 = (dmu * out_std) * (1.0f - t * t);
       } else {
-        float t = tanhf(y);
-        float mu = t * out_std + out_mean;
-        float a = rt - slot[IN_S0 + 32 + j];
-        float A = (a - meanf) / (stdf + 1e-10f);
-        float diff = (float)((double)slot[IN_S1 + j] - (double)mu);
-        float x = diff * MVN_INV_L;
-        float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-        double r = exp((double)lp - (double)slot[IN_S1 + 32 + j]);
-        double Ad = (double)A;
-        double rc = r < 0.8 ? 0.8 : (r > 1.2 ? 1.2 : r);
-        double s1 = r * Ad, s2 = rc * Ad, in = (r >= 0.8 && r <= 1.2) ? 1.0 : 0.0;
-        double g = (s1 < s2) ? Ad : ((s2 < s1) ? in * Ad : 0.5 * Ad + 0.5 * in * Ad);
-        if (kh == 0) dacc[0] += -(s1 < s2 ? s1 : s2);
-        float dmu = (float)(inv_m * (-g) * r * (double)x * (double)MVN_INV_L);
-        dy = (dmu * out_std) * (1.0f - t * t);
+        // softmax over the pair (as torch: shift by the max), pn = p / (p0 + p1)
+        const float mx = fmaxf(y0, y1);
+        const float e0 = expf(y0 - mx), e1 = expf(y1 - mx);
+        const float se = e0 + e1;
+        const float p[2] = {e0 / se, e1 / se};
+        const float a = rt - slot[LY::IN_S0 + 32 + j];
+        const float A = (a - meanf) / (stdf + 1e-10f);
+        const double old = (double)slot[LY::IN_S1 + j];
+        const float sp = p[0] + p[1];
+        const float pn[2] = {p[0] / sp, p[1] / sp};
+        const float eps = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
+        const double inv_m2 = inv_m * inv_m;
+        double dlp[2], f = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const float pc = pn[k] < eps ? eps : (pn[k] > hi ? hi : pn[k]);
+          const double r = exp((double)logf(pc) - old);
+          double dfdr;
+          f += counts[k] * surr_and_grad(r, (double)A, dfdr);
+          const double pass = (pn[k] >= eps && pn[k] <= hi) ? 1.0 : 0.0;
+          dlp[k] = inv_m2 * counts[k] * dfdr * r * pass / (double)pc;  // dL/dpn_k
+        }
+        if (kh == 0) dacc[0] += f;
+        const double sd = (double)sp;
+        const double g0 = (dlp[0] * (1.0 - pn[0]) - dlp[1] * pn[1]) / sd;  // dL/dp_k
+        const double g1 = (dlp[1] * (1.0 - pn[1]) - dlp[0] * pn[0]) / sd;
+        const double dot = (double)p[0] * g0 + (double)p[1] * g1;
+        dy0 = (float)((double)p[0] * (g0 - dot));  // softmax Jacobian
+        dy1 = (float)((double)p[1] * (g1 - dot));
       }
     }
-    gB4 += (kh == 0) ? dy : 0.0f;
-    // ---- layer 4 backward: dW4 = rowsum(dy * h3), dH3 = w4 * dy masked
-    f32x16 g = zero16();
+    gB40 += (kh == 0) ? dy0 : 0.0f;
+    gB41 += (kh == 0) ? dy1 : 0.0f;
+    // ---- layer 4 backward: dW4 = rowsum(dy * h3), dH3 = W4^T dy masked
+    f32x16 g = zero16(), g1v = zero16();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      float4 c = reinterpret_cast<const float4 *>(lds + O_W4)[2 * q + kh];
+      float4 c = reinterpret_cast<const float4 *>(lds + LY::O_W4)[2 * q + kh];
       float cw[4] = {c.x, c.y, c.z, c.w};
+      float cw1[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (NOUT == 2) {
+        float4 c1 = reinterpret_cast<const float4 *>(lds + LY::O_W4 + 32)[2 * q + kh];
+        cw1[0] = c1.x, cw1[1] = c1.y, cw1[2] = c1.z, cw1[3] = c1.w;
+      }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int r = 4 * q + i;
-        g[r] = dy * h3[r];
-        h3[r] = (h3[r] > 0.0f) ? cw[i] * dy : 0.0f;  // h3 := dH3^T
+        g[r] = dy0 * h3[r];
+        if constexpr (NOUT == 2) {
+          g1v[r] = dy1 * h3[r];
+          h3[r] = (h3[r] > 0.0f) ? fmaf(cw1[i], dy1, cw[i] * dy0) : 0.0f;  // h3 := dH3^T
+        } else {
+          h3[r] = (h3[r] > 0.0f) ? cw[i] * dy0 : 0.0f;
+        }
       }
     }
     put_tile(T0, g, l);
@@ -349,8 +427,14 @@ __global__ void __launch_bounds__(64 * WAVES)
     wave_sync();
     phase();
     if (kh == 0) {
-      gW4 += row_sum(T0, l);
+      gW40 += row_sum(T0, l);
       gB3 += row_sum(T1, l);
+    }
+    if constexpr (NOUT == 2) {
+      wave_sync();
+      put_tile(T0, g1v, l);
+      wave_sync();
+      if (kh == 0) gW41 += row_sum(T0, l);
     }
     wave_sync();
     phase();
@@ -373,8 +457,8 @@ __global__ void __launch_bounds__(64 * WAVES)
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int f = feat(s, l);
-      d2a = mfma(lds[O_W3 + f * S3 + j], h3[s], d2a);
-      d2b = mfma(lds[O_W3 + f * S3 + 32 + j], h3[s], d2b);
+      d2a = mfma(lds[LY::O_W3 + f * S3 + j], h3[s], d2a);
+      d2b = mfma(lds[LY::O_W3 + f * S3 + 32 + j], h3[s], d2b);
     }
 #pragma unroll
     for (int r = 0; r < 16; r++) {
@@ -400,9 +484,9 @@ __global__ void __launch_bounds__(64 * WAVES)
     // dH1^T = W2^T . dH2^T, masked by h1 > 0
     f32x16 d1 = zero16();
 #pragma unroll
-    for (int s = 0; s < 16; s++) d1 = mfma(lds[O_W2 + feat(s, l) * S2 + j], d2a[s], d1);
+    for (int s = 0; s < 16; s++) d1 = mfma(lds[LY::O_W2 + feat(s, l) * S2 + j], d2a[s], d1);
 #pragma unroll
-    for (int s = 0; s < 16; s++) d1 = mfma(lds[O_W2 + (32 + feat(s, l)) * S2 + j], d2b[s], d1);
+    for (int s = 0; s < 16; s++) d1 = mfma(lds[LY::O_W2 + (32 + feat(s, l)) * S2 + j], d2b[s], d1);
 #pragma unroll
     for (int r = 0; r < 16; r++) d1[r] = (h1[r] > 0.0f) ? d1[r] : 0.0f;
     wave_sync();
@@ -415,18 +499,18 @@ __global__ void __launch_bounds__(64 * WAVES)
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int k = 2 * s + kh;
-      float b = (j < NIN) ? Xs[k * NIN + j] : 0.0f;
+      float b = (j < nin) ? Xs[k * nin + j] : 0.0f;
       gW1 = mfma(T0[j * ST + k], b, gW1);
     }
     wave_sync();
     phase();
   }
   // ---- write this wave's partial gradient (packed torch layout)
-  float *gp = gpart + (size_t)gw * NW;
+  float *gp = gpart + (size_t)gw * NWP;
 #pragma unroll
   for (int r = 0; r < 16; r++) {
     int f = feat(r, l);
-    if (j < NIN) gp[G_W1 + f * NIN + j] = gW1[r];
+    if (j < nin) gp[G_W1 + f * nin + j] = gW1[r];
     gp[G_W2 + f * 32 + j] = gW2a[r];
     gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
     gp[G_W3 + f * 64 + j] = gW3a[r];
@@ -435,13 +519,17 @@ __global__ void __launch_bounds__(64 * WAVES)
   if (kh == 0) {
     gp[G_B1 + j] = gB1;
     gp[G_B3 + j] = gB3;
-    gp[G_W4 + j] = gW4;
+    gp[G_W4 + j] = gW40;
+    if (NOUT == 2) gp[G_W4 + 32 + j] = gW41;
   }
   gp[G_B2 + l] = gB2;  // lanes 0-31: features 0-31 (T0), lanes 32-63: 32-63 (T1)
   // b4 and float64 sums: wave reductions
-  float b4s = gB4;
+  float b4s0 = gB40, b4s1 = gB41;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) b4s += __shfl_xor(b4s, o);
+  for (int o = 32; o > 0; o >>= 1) {
+    b4s0 += __shfl_xor(b4s0, o);
+    b4s1 += __shfl_xor(b4s1, o);
+  }
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (kh == 0) s0 = dacc[0], s1 = dacc[32], s2 = dacc[64];
 #pragma unroll
@@ -451,7 +539,8 @@ __global__ void __launch_bounds__(64 * WAVES)
     s2 += __shfl_xor(s2, o);
   }
   if (l == 0) {
-    gp[G_B4] = b4s;
+    gp[G_B4] = b4s0;
+    if (NOUT == 2) gp[G_B4 + 1] = b4s1;
     dpart[gw * 3 + 0] = s0;
     dpart[gw * 3 + 1] = s1;
     dpart[gw * 3 + 2] = s2;
@@ -460,35 +549,35 @@ __global__ void __launch_bounds__(64 * WAVES)
 
 // Deterministic two-stage gradient reduction over the per-wave partials (fixed order,
 // float64): stage 1 sums contiguous groups of waves, stage 2 sums the RG group totals.
+// Slot k < np is gradient k, slots np..np+2 the float64 sums.
 constexpr int RG = 32;
-constexpr int NWD = NW + 3;  // gradient + (loss, sum A, sum A^2)
 
 __global__ void __launch_bounds__(256)
-    k_grad_stage1(const float *gpart, const double *dpart, int nw, double *tmp) {
-  int k = blockIdx.x * 256 + threadIdx.x;
-  int g = blockIdx.y;
-  int i0 = (int)((int64_t)g * nw / RG), i1 = (int)((int64_t)(g + 1) * nw / RG);
+    k_grad_stage1(const float *gpart, const double *dpart, int nw, int np, double *tmp) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y, nd = np + 3;
+  const int i0 = (int)((int64_t)g * nw / RG), i1 = (int)((int64_t)(g + 1) * nw / RG);
   double s = 0.0;
-  if (k < NW) {
-    for (int i = i0; i < i1; i++) s += (double)gpart[(size_t)i * NW + k];
-  } else if (k < NWD) {
-    for (int i = i0; i < i1; i++) s += dpart[(size_t)i * 3 + (k - NW)];
+  if (k < np) {
+    for (int i = i0; i < i1; i++) s += (double)gpart[(size_t)i * np + k];
+  } else if (k < nd) {
+    for (int i = i0; i < i1; i++) s += dpart[(size_t)i * 3 + (k - np)];
   } else {
     return;
   }
-  tmp[(size_t)g * NWD + k] = s;
+  tmp[(size_t)g * nd + k] = s;
 }
 
-__global__ void __launch_bounds__(256) k_grad_stage2(const double *tmp, float *grad, double *out3) {
-  int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= NWD) return;
+__global__ void __launch_bounds__(256) k_grad_stage2(const double *tmp, int np, float *grad, double *out3) {
+  const int k = blockIdx.x * 256 + threadIdx.x, nd = np + 3;
+  if (k >= nd) return;
   double s = 0.0;
 #pragma unroll 8
-  for (int g = 0; g < RG; g++) s += tmp[(size_t)g * NWD + k];
-  if (k < NW)
+  for (int g = 0; g < RG; g++) s += tmp[(size_t)g * nd + k];
+  if (k < np)
     grad[k] = (float)s;
   else if (out3)
-    out3[k - NW] += s;
+    out3[k - np] += s;
 }
 
 struct Work {  // per-device partial buffers (calls on one device must share one stream)
@@ -496,54 +585,83 @@ struct Work {  // per-device partial buffers (calls on one device must share one
   double *d = nullptr;
   double *t = nullptr;
   int nw = 0;
+  int cus = 0;
 };
 Work g_work[16];
 
-int grid_waves() {
-  int dev = 0, cus = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return cus * WAVES;  // one block of 8 waves per CU
+template <int KIND, int KS, bool PF>
+void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int nin, int64_t M, const float *ret,
+            float *value, const float *act, const float *logp_old, const double *stats, const double *counts,
+            double m_global, float out_mean, float out_std, float *gp, double *dp) {
+  using LY = Lay<KS, PF, (KIND == K_CHOICE ? 2 : 1)>;
+  hipLaunchKernelGGL((k_mlp_train<KIND, KS, PF>), grid, dim3(64 * LY::WAVES), sizeof(float) * LY::FLOATS, s,
+                     packed, X, nin, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, gp, dp);
 }
 }  // namespace
 
-extern "C" int mhppo_mlp_train_cont(int kind, const float *packed, const float *X, int64_t M, const float *ret,
-                                    float *value, const float *act, const float *logp_old, const double *stats,
-                                    double m_global, float out_mean, float out_std, float *grad, double *sums,
-                                    void *stream) {
-  if (!packed || !X || !ret || !value || !grad || M < 0 || (kind != 0 && kind != 1))
-    return set_error(MHPPO_EINVAL, "bad argument");
-  if (kind == 1 && (!act || !logp_old || !stats)) return set_error(MHPPO_EINVAL, "actor pass needs act/logp/stats");
-  if (((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
+extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const float *X, int64_t M, const float *ret,
+                               float *value, const float *act, const float *logp_old, const double *stats,
+                               const double *counts, double m_global, float out_mean, float out_std, float *grad,
+                               double *sums, void *stream) {
+  if (!packed || !X || !ret || !value || !grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 ||
+      n_in > 32)
+    return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= 32)");
+  if (kind == K_CONT && (n_in != NIN_CONT || !act || !logp_old || !stats))
+    return set_error(MHPPO_EINVAL, "continuous actor pass needs n_in 13 and act/logp_old/stats");
+  if (kind == K_CHOICE && (!logp_old || !stats || !counts))
+    return set_error(MHPPO_EINVAL, "choice actor pass needs logp_old/stats/counts");
+  if (M > ((int64_t)1 << 40)) return set_error(MHPPO_EINVAL, "M too large");
+  const bool pf = n_in == NIN_CONT && kind != K_CHOICE;
+  if (pf && ((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
   Work &wk = g_work[dev & 15];
-  int nw = grid_waves();
-  if (M > 0) nw = (int)min((int64_t)nw, ((M + 31) / 32 + WAVES - 1) / WAVES * WAVES);
-  if (nw < WAVES) nw = WAVES;
+  if (wk.cus == 0) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    wk.cus = cus;
+  }
+  const int waves = pf ? 8 : 4;
+  int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
+  const int64_t tiles = (M + 31) / 32;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
+  const int nw = (int)blocks * waves;
   if (wk.nw < nw) {
     if (wk.g) (void)hipFree(wk.g);
     if (wk.d) (void)hipFree(wk.d);
     if (wk.t) (void)hipFree(wk.t);
-    if (hipMalloc(&wk.g, sizeof(float) * (size_t)nw * NW) != hipSuccess ||
+    if (hipMalloc(&wk.g, sizeof(float) * (size_t)nw * NW_MAX) != hipSuccess ||
         hipMalloc(&wk.d, sizeof(double) * (size_t)nw * 3) != hipSuccess ||
-        hipMalloc(&wk.t, sizeof(double) * (size_t)RG * NWD) != hipSuccess) {
+        hipMalloc(&wk.t, sizeof(double) * (size_t)RG * (NW_MAX + 3)) != hipSuccess) {
       wk = Work{};
       return set_error(MHPPO_ENOMEM, "mlp_train partials");
     }
     wk.nw = nw;
   }
-  dim3 grid(nw / WAVES), blk(64 * WAVES);
-  size_t shm = sizeof(float) * LDS_FLOATS;
-  if (kind == 0)
-    hipLaunchKernelGGL(k_mlp_train<0>, grid, blk, shm, s, packed, X, M, ret, value, act, logp_old, stats, m_global,
-                       out_mean, out_std, wk.g, wk.d);
-  else
-    hipLaunchKernelGGL(k_mlp_train<1>, grid, blk, shm, s, packed, X, M, ret, value, act, logp_old, stats, m_global,
-                       out_mean, out_std, wk.g, wk.d);
-  hipLaunchKernelGGL(k_grad_stage1, dim3((NWD + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, wk.t);
-  hipLaunchKernelGGL(k_grad_stage2, dim3((NWD + 255) / 256), dim3(256), 0, s, wk.t, grad, sums);
+  const dim3 grid((unsigned)blocks);
+#define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
+  if (pf) {
+    if (kind == K_CRITIC)
+      launch<K_CRITIC, 7, true>(MLP_ARGS);
+    else
+      launch<K_CONT, 7, true>(MLP_ARGS);
+  } else {
+    const int ks = n_in <= 16 ? 8 : (n_in <= 24 ? 12 : 16);
+    if (kind == K_CRITIC) {
+      if (ks == 8) launch<K_CRITIC, 8, false>(MLP_ARGS);
+      else if (ks == 12) launch<K_CRITIC, 12, false>(MLP_ARGS);
+      else launch<K_CRITIC, 16, false>(MLP_ARGS);
+    } else {
+      if (ks == 8) launch<K_CHOICE, 8, false>(MLP_ARGS);
+      else if (ks == 12) launch<K_CHOICE, 12, false>(MLP_ARGS);
+      else launch<K_CHOICE, 16, false>(MLP_ARGS);
+    }
+  }
+#undef MLP_ARGS
+  const int np = n_params(n_in, kind == K_CHOICE ? 2 : 1);
+  hipLaunchKernelGGL(k_grad_stage1, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, np, wk.t);
+  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

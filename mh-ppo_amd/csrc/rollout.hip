@@ -250,20 +250,6 @@ __global__ void __launch_bounds__(TPB)
   adv[i] = (a - meanf) / (stdf + 1e-10f);
 }
 
-// d/dr of -min(r A, clamp(r, .8, 1.2) A) with torch's tie rule (minimum splits the
-// gradient evenly on ties; clamp passes it on [0.8, 1.2] inclusive)
-__device__ inline double surr_and_grad(double r, double A, double &dfdr) {
-  double rc = r < 0.8 ? 0.8 : (r > 1.2 ? 1.2 : r);
-  double s1 = r * A, s2 = rc * A;
-  double in = (r >= 0.8 && r <= 1.2) ? 1.0 : 0.0;
-  double g;
-  if (s1 < s2) g = A;
-  else if (s2 < s1) g = in * A;
-  else g = 0.5 * A + 0.5 * in * A;
-  dfdr = -g;
-  return -(s1 < s2 ? s1 : s2);
-}
-
 __global__ void __launch_bounds__(TPB)
     k_ppo_cont(const float *mu, const float *act, const float *lp_old, const float *adv, int64_t M, double inv_m,
                float *dmu, double *partials) {

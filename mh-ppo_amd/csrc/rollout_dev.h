@@ -222,6 +222,24 @@ MHPPO_HD inline void mlp_forward(const float *W, int n_in, const float *x, float
 // (multivariate_normal.py rsample/log_prob; pinned in tests/test_rollout_math.py):
 //   sample a = loc + L*eps;  x = (a - loc) * (1/L);  logp = -0.5*(log(2 pi) + x*x) - log(L)
 constexpr float MVN_L = 0x1.6a09e6p-1f;        // cholesky([[0.5]]) in float32
+// PPO clipped surrogate f = -min(r A, clamp(r, .8, 1.2) A) and df/dr, with torch's tie
+// rule (minimum splits the gradient evenly on ties; clamp passes it on [0.8, 1.2]
+// inclusive) — Coop-MH-PPO-scalable.py:803-806, :838-841
+MHPPO_HD inline double surr_and_grad(double r, double A, double &dfdr) {
+  double rc = r < 0.8 ? 0.8 : (r > 1.2 ? 1.2 : r);
+  double s1 = r * A, s2 = rc * A;
+  double in = (r >= 0.8 && r <= 1.2) ? 1.0 : 0.0;
+  double g;
+  if (s1 < s2)
+    g = A;
+  else if (s2 < s1)
+    g = in * A;
+  else
+    g = 0.5 * A + 0.5 * in * A;
+  dfdr = -g;
+  return -(s1 < s2 ? s1 : s2);
+}
+
 constexpr float MVN_INV_L = 0x1.6a09e6p+0f;    // float32(1/L) as torch's triangular solve uses
 constexpr float MVN_LOG2PI = 0x1.d67f1cp+0f;   // float32(1 * math.log(2*math.pi))
 constexpr float MVN_HALF_LOGDET = -0x1.62e432p-2f;  // float32 log(L)

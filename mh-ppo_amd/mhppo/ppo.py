@@ -102,43 +102,60 @@ def k_ppo_choice(probs, logp_old, adv, counts, m_global):
 
 
 # Optional launch timing (bench.py): when a list, each fused train launch appends
-# (kind, rows, start_event, end_event) recorded on the launch stream.
+# (kind, n_in, rows, start_event, end_event) recorded on the launch stream.
 TRAIN_EVENTS = None
 
-# Algorithmic FLOPs of one row through the fused kernel:
-# forward 2*4544, backward data (no dX) 2*(32 + 2048 + 2048), weight grads 2*4544.
-FLOPS_PER_ROW_CONT = 2 * 4544 + 2 * (32 + 2048 + 2048) + 2 * 4544
 
-N_PARAMS_CONT = 13 * 32 + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 + 1  # 4673
+def flops_per_row(n_in, n_out):
+    """Algorithmic FLOPs of one row through the fused kernel: forward and
+    weight gradient 2 * (32 n_in + 2048 + 2048 + 32 n_out) each, backward data without
+    dX 2 * (32 n_out + 2048 + 2048).  13 -> 1: 26,432."""
+    macs = 32 * n_in + 2048 + 2048 + 32 * n_out
+    return 2 * macs + 2 * (32 * n_out + 4096) + 2 * macs
 
 
-def k_mlp_train_cont(kind, net, obs, ret, value, act, logp_old, stats, m_global):
-    """Fused forward/loss/backward of a continuous-head net (mhppo_mlp_train_cont).
-    kind 0 (critic): returns (grad[4673], sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
-    kind 1 (actor):  returns (grad[4673], sums[3] = (sum clip-surrogate, 0, 0), None)."""
-    if net.n_in != 13 or net.n_out != 1 or (kind == 0) != (net.model_type == 0):
-        raise ValueError("fused continuous-head kernel needs a 13->1 Model_PPO of the matching kind")
+FLOPS_PER_ROW_CONT = flops_per_row(13, 1)
+
+KIND_CRITIC, KIND_CONT, KIND_CHOICE = 0, 1, 2
+
+
+def n_params(n_in, n_out):
+    return 32 * n_in + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 * n_out + n_out
+
+
+def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=None, counts=None, m_global=1.0):
+    """Fused forward/loss/backward of one head (mhppo_mlp_train).
+    kind 0 (critic): returns (grad, sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
+    kind 1 (continuous actor) / 2 (choice actor): returns (grad, sums[3] = (sum surrogate, 0, 0), None).
+    grad is the packed torch-layout gradient (W1 b1 .. W4 b4)."""
+    want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
+    if net.model_type != want or net.n_in > 32 or (kind == KIND_CONT and net.n_in != 13):
+        raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
+                         f"{net.n_in}->{net.n_out} Model_PPO")
     dev = obs.device
     M = obs.shape[0]
-    V = torch.empty(M, dtype=torch.float32, device=dev) if kind == 0 else value.detach().contiguous()
-    grad = torch.empty(N_PARAMS_CONT, dtype=torch.float32, device=dev)
-    sums = torch.zeros(3, dtype=torch.float64, device=dev)
-    obs, ret = obs.float().contiguous(), ret.float().contiguous()
+    obs = obs.float().contiguous()
+    if obs.data_ptr() % 16:
+        obs = obs.clone()
+    ret = ret.float().contiguous()
+    V = torch.empty(M, dtype=torch.float32, device=dev) if kind == KIND_CRITIC else value.detach().float().contiguous()
     act = None if act is None else act.float().contiguous()
     logp_old = None if logp_old is None else logp_old.float().contiguous()
+    grad = torch.empty(n_params(net.n_in, net.n_out), dtype=torch.float32, device=dev)
+    sums = torch.zeros(3, dtype=torch.float64, device=dev)
     w = net.packed()
     p = _lib.ptr
     ev = None
     if TRAIN_EVENTS is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    _lib.check(_lib.lib().mhppo_mlp_train_cont(
-        kind, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), float(m_global),
+    _lib.check(_lib.lib().mhppo_mlp_train(
+        kind, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts), float(m_global),
         float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
     if ev is not None:
         ev[1].record()
-        TRAIN_EVENTS.append((kind, M, ev[0], ev[1]))
-    return grad, sums, (V if kind == 0 else None)
+        TRAIN_EVENTS.append((kind, net.n_in, M, ev[0], ev[1]))
+    return grad, sums, (V if kind == KIND_CRITIC else None)
 
 
 # ------------------------------------------------------------- DP orchestration
@@ -166,9 +183,9 @@ def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
     critic pass (V, MSE gradient, advantage sums) -> all-reduce of the sums -> actor pass
     (clip-surrogate gradient w.r.t. the start-of-epoch critic's advantage) -> one gradient
     all-reduce -> Adam.  Returns this rank's (actor, critic) loss sums (float64 tensors)."""
-    gc, sc, V = k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, m_global)
+    gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
     stats = _allreduce_(sc[1:3].clone())
-    ga, sa, _ = k_mlp_train_cont(1, actor, obs, ret, V, act, logp_old, stats, m_global)
+    ga, sa, _ = k_mlp_train(KIND_CONT, actor, obs, ret, V, act, logp_old, stats, m_global=m_global)
     _set_grads(critic, gc)
     _set_grads(actor, ga)
     _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
@@ -195,7 +212,28 @@ def train_model_c_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_
 
 
 def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts):
-    """One full-batch epoch of Algo_PPO.train_model_d (:818-851); counts = global (n0, n1) float64."""
+    """One full-batch epoch of Algo_PPO.train_model_d (:818-851) on the fused kernel:
+    critic pass -> all-reduce of the advantage sums -> choice-actor pass (O(M) form of the
+    M x M Categorical surrogate with the global action counts) -> gradient all-reduce ->
+    Adam.  counts = global (n0, n1) float64.  Returns this rank's (actor, critic) loss sums."""
+    if critic.n_in > 32:
+        return train_model_d_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global,
+                                      counts)
+    gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
+    stats = _allreduce_(sc[1:3].clone())
+    ga, sa, _ = k_mlp_train(KIND_CHOICE, actor, obs, ret, V, None, logp_old, stats, counts.double().contiguous(),
+                            m_global=m_global)
+    _set_grads(critic, gc)
+    _set_grads(actor, ga)
+    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+    opt_actor.step()
+    opt_critic.step()
+    return sa[0:1], sc[0:1]
+
+
+def train_model_d_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts):
+    """train_model_d with the MLPs in PyTorch autograd and the PPO arithmetic in HIP (choice
+    observations wider than the fused kernel's 32 inputs; cross-check for the fused kernel)."""
     V = torch.squeeze(critic(obs), -1)
     adv = normalized_advantage(ret, V, m_global)
     probs = actor(obs).reshape(-1, 2)

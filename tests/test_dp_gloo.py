@@ -49,7 +49,8 @@ def _install_cpu_doubles(ppo):
         dmu = (1.0 / m) * (-g) * r * x.double() / L
         return dmu.float(), (-torch.minimum(s1, s2)).sum().reshape(1)
 
-    def mlp_train_cont(kind, net, obs, ret, value, act, lp_old, stats, m):
+    def mlp_train(kind, net, obs, ret, value=None, act=None, lp_old=None, stats=None, counts=None, m_global=1.0):
+        m = m_global
         params = list(net.parameters())
         out = torch.squeeze(net(obs), -1)
         if kind == 0:
@@ -64,7 +65,7 @@ def _install_cpu_doubles(ppo):
         return torch.cat([x.reshape(-1) for x in g]), torch.cat([loss, torch.zeros(2, dtype=torch.float64)]), None
 
     ppo.k_adv_stats, ppo.k_adv_normalize, ppo.k_mse, ppo.k_ppo_cont = adv_stats, adv_normalize, mse, ppo_cont
-    ppo.k_mlp_train_cont = mlp_train_cont
+    ppo.k_mlp_train = mlp_train
 
 
 def _run(rank, world, port, data, out_q):

@@ -80,11 +80,28 @@ def test_philox_noise_moments():
     assert torch.equal(y, x[5000:6000])
 
 
+def _close_grad(g, gt):
+    torch.testing.assert_close(g, gt, rtol=0, atol=1e-4 * float(gt.abs().max()) + 1e-9)
+
+
+def _critic_pass(ppo, critic, obs, ret, m):
+    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+    Vt = torch.squeeze(critic(obs), -1)
+    torch.testing.assert_close(V, Vt.detach(), rtol=1e-5, atol=1e-5)
+    dv, lc = ppo.k_mse(Vt, ret, m)
+    st = ppo.k_adv_stats(ret, Vt)
+    gct = torch.cat([g.reshape(-1) for g in torch.autograd.grad(Vt, list(critic.parameters()), dv)])
+    assert abs(float(sc[0]) - float(lc[0])) <= 1e-5 * abs(float(lc[0])) + 1e-6
+    torch.testing.assert_close(sc[1:3], st, rtol=1e-5, atol=1e-3)
+    _close_grad(gc, gct)
+    return Vt, st
+
+
 @pytest.mark.parametrize("M", [1, 31, 33, 1000, 70001])
 def test_fused_cont_grads_vs_autograd(M):
-    """mhppo_mlp_train_cont (fused MFMA forward/backward) vs torch autograd of the same
-    losses on the same weights: V bit-close, loss sums 1e-5 rel, gradients within 1e-4 of
-    the gradient's max-abs (fp32 accumulation order differs)."""
+    """mhppo_mlp_train kinds 0/1 (fused MFMA forward/backward, 13 inputs, DMA-prefetch
+    path) vs torch autograd of the same losses on the same weights: V 1e-5, loss sums
+    1e-5 rel, gradients within 1e-4 of the gradient's max-abs (fp32 summation order)."""
     from mhppo import ppo
     from mhppo.models import Model_PPO
     torch.manual_seed(M)
@@ -95,20 +112,36 @@ def test_fused_cont_grads_vs_autograd(M):
     act = (torch.randn(M) - 1).cuda()
     lp = (torch.randn(M) * 0.3 - 0.9).cuda()
     m = float(M) if M > 1 else 2.0  # unbiased std needs m > 1
-    gc, sc, V = ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, m)
-    Vt = torch.squeeze(critic(obs), -1)
-    torch.testing.assert_close(V, Vt.detach(), rtol=1e-5, atol=1e-5)
-    dv, lc = ppo.k_mse(Vt, ret, m)
-    st = ppo.k_adv_stats(ret, Vt)
-    gct = torch.cat([g.reshape(-1) for g in torch.autograd.grad(Vt, list(critic.parameters()), dv)])
-    assert abs(float(sc[0]) - float(lc[0])) <= 1e-5 * abs(float(lc[0])) + 1e-6
-    torch.testing.assert_close(sc[1:3], st, rtol=1e-5, atol=1e-3)
-    torch.testing.assert_close(gc, gct, rtol=0, atol=1e-4 * float(gct.abs().max()) + 1e-9)
-    stats = st
-    ga, sa, _ = ppo.k_mlp_train_cont(1, actor, obs, ret, Vt, act, lp, stats, m)
+    Vt, st = _critic_pass(ppo, critic, obs, ret, m)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, Vt, act, lp, st, m_global=m)
     mu = torch.squeeze(actor(obs), -1)
-    adv = ppo.k_adv_normalize(ret, Vt, stats, m)
+    adv = ppo.k_adv_normalize(ret, Vt, st, m)
     dmu, la = ppo.k_ppo_cont(mu, act, lp, adv, m)
     gat = torch.cat([g.reshape(-1) for g in torch.autograd.grad(mu, list(actor.parameters()), dmu)])
     assert abs(float(sa[0]) - float(la[0])) <= 1e-5 * abs(float(la[0])) + 1e-6
-    torch.testing.assert_close(ga, gat, rtol=0, atol=1e-4 * float(gat.abs().max()) + 1e-9)
+    _close_grad(ga, gat)
+
+
+@pytest.mark.parametrize("M,dc", [(1, 12), (45, 17), (4096, 27), (20001, 30), (333, 32)])
+def test_fused_choice_grads_vs_autograd(M, dc):
+    """mhppo_mlp_train kinds 0/2 on choice-head shapes (dc = 12..32 inputs, 2-way softmax,
+    O(M) count-weighted surrogate) vs torch autograd + the HIP choice-loss kernel."""
+    from mhppo import ppo
+    from mhppo.models import Model_PPO
+    torch.manual_seed(M + dc)
+    actor = Model_PPO(dc, 2, 2).cuda()
+    critic = Model_PPO(dc, 1, 0).cuda()
+    obs = (torch.randn(M, dc) * 2).cuda()
+    ret = (torch.randn(M) * 3 - 5).cuda()
+    act = (torch.rand(M) < 0.4).float().cuda()
+    lp = torch.log(torch.rand(M) * 0.8 + 0.1).cuda()
+    m = float(M) if M > 1 else 2.0
+    counts = torch.tensor([float((act == 0).sum()), float((act == 1).sum())], dtype=torch.float64).cuda()
+    Vt, st = _critic_pass(ppo, critic, obs, ret, m)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CHOICE, actor, obs, ret, Vt, None, lp, st, counts, m_global=m)
+    probs = actor(obs).reshape(-1, 2)
+    adv = ppo.k_adv_normalize(ret, Vt, st, m)
+    dp, la = ppo.k_ppo_choice(probs, lp, adv, counts, m)
+    gat = torch.cat([g.reshape(-1) for g in torch.autograd.grad(probs, list(actor.parameters()), dp)])
+    assert abs(float(sa[0]) - float(la[0])) <= 1e-5 * abs(float(la[0])) + 1e-6
+    _close_grad(ga, gat)

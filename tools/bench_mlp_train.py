@@ -24,18 +24,18 @@ ret = torch.randn(M, device="cuda") * 8 - 20
 act = torch.randn(M, device="cuda") - 1
 lp = torch.randn(M, device="cuda") * 0.3 - 0.9
 for kind in (0, 1, 0, 1):
-    gc, sc, V = ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, float(M))
-    ga, sa, _ = ppo.k_mlp_train_cont(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), float(M))
+    gc, sc, V = ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M))
+    ga, sa, _ = ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M))
 torch.cuda.synchronize()
 for kind in (0, 1):
     ppo.TRAIN_EVENTS = []
     for _ in range(a.reps):
         if kind == 0:
-            ppo.k_mlp_train_cont(0, critic, obs, ret, None, None, None, None, float(M))
+            ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M))
         else:
-            ppo.k_mlp_train_cont(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), float(M))
+            ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M))
     torch.cuda.synchronize()
-    ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
+    ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
     tf = ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12
     print(f"kind {kind} rows {M}: {ms:.3f} ms  {tf:.1f} TFLOP/s "
           f"({100 * tf / 157.3:.1f}% of f32 MFMA peak)", flush=True)
