@@ -48,6 +48,21 @@ def env_step_bytes(S, nC, P, obs_dim, T=80):
     return car + ped + env + io_in + io_out
 
 
+def pmc_traffic(*patterns):
+    """Mean HBM bytes per launch over the kernels matching `patterns`, from the committed
+    rocprofv3 PMC summary (profiles/pmc_traffic.json, made by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this bench; reads = 2 x FETCH_SIZE on
+    gfx950).  None when absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    vals = [v["hbm_bytes_per_launch"] for k, v in ks.items()
+            if any(p in k for p in patterns) and v.get("hbm_bytes_per_launch")]
+    return sum(vals) / len(vals) if vals else None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,8 +162,8 @@ def main():
     tr_rows = sum(m for _, _, m, _, _ in tr)
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
-    traffic = os.environ.get("MHPPO_PMC_BYTES_PER_LAUNCH")
-    traffic_env = os.environ.get("MHPPO_PMC_BYTES_PER_ENV_LAUNCH")
+    traffic = pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>")
+    traffic_env = pmc_traffic("k_sample_env<")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -159,12 +174,13 @@ def main():
                    "envs_per_gpu": N, "agents": S, "T": T, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": "k_mlp_train (fused continuous-head fwd/loss/bwd/wgrad, f32 MFMA)",
                      "achieved": tr_tflops, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": tr_tflops / F32_MFMA_PEAK_TFLOPS, "traffic": float(traffic) if traffic else None,
+                     "frac": tr_tflops / F32_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "B/launch",
                      "flops_per_row": ppo.FLOPS_PER_ROW_CONT, "rows_per_launch": tr_rows / max(len(tr), 1),
                      "launches": len(tr), "launch_ms": tr_ms / max(len(tr), 1)},
         "roofline_env": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": float(traffic_env) if traffic_env else None, "bytes_per_env_step": per_env,
+                         "traffic": traffic_env, "traffic_unit": "B/launch",
+                         "bytes_per_launch": per_env * N, "bytes_per_env_step": per_env,
                          "kernel_ms": kern_ms},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
