@@ -108,6 +108,29 @@ typedef struct mhppo_rollout_bufs {
 
 int mhppo_choice_dim(const mhppo_env *env);
 
+/* Deterministic evaluation (Env_rollout.iterations :152-252, run by Algo_PPO.evaluate
+ * :738-747).  Device buffers; per-step outputs are time-major [T][N][..]. */
+typedef struct mhppo_eval_bufs {
+    float *obs;       /* [N, obs_dim] current observation (in/out; mhppo_env_reset fills it) */
+    int32_t *a_d;     /* [N, S, P] current choice (argmax of the choice actor) */
+    uint8_t *trig;    /* [N] re-decision due at the next step */
+    double *ep_min;   /* [N, S] episodic min of reward_light since the last decision */
+    float *obs_hist;  /* [T, N, obs_dim] pre-step observations (batch_obs) */
+    float *acts;      /* [T, N, S] continuous actions (batch_acts) */
+    float *rews_c;    /* [T, N, S] step rewards (batch_rews_c) */
+    float *rews_d;    /* [T, N, S] episodic reward at a save (batch_rews_d), rows with saved = 1 */
+    float *waiting;   /* [T, N, P] pedestrians' waiting_time at a save, rows with saved = 1 */
+    uint8_t *saved;   /* [T, N] a save happened after step t (re-decision or done) */
+    int32_t T, reserved;
+} mhppo_eval_bufs;
+
+/* Step t of an evaluation episode in every env (t = 0 right after mhppo_env_reset):
+ * choice argmax when a decision is due (t = 0 or the re-decision test fired), per car
+ * a = min over pedestrians of the head's mean action (left-lane pedestrians: clamped
+ * speed-limit tracking), capped by (10 - V)/dt; lights = 2 a_d[flat i] - 1; env step. */
+int mhppo_eval_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                    const mhppo_mlp *actor_choice, int t, mhppo_eval_bufs *bufs, void *stream);
+
 /* Episode start (:377-428): reset every env, write obs, choice features obs_car_ped_d
  * (:574-611) and closest pedestrian (:614-627), run the choice actor and draw
  * Categorical samples.  When `forced_a` (int32 [N,S,P]) is non-NULL the draws are

@@ -155,6 +155,92 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
+// -------------------------------------------------------------- evaluation
+// Env_rollout.iterations (:152-252; the routine Algo_PPO.evaluate runs), one lane per env
+// and step: deterministic choice (argmax) when a decision is due, mean actions with the
+// left-lane override and the (10 - V)/dt cap, the flat-index light quirk, env step,
+// episodic min, re-decision test and saves.  Weights of the three heads in LDS.
+template <int V>
+__global__ void __launch_bounds__(TPB) k_eval_step(Cfg c, Bufs eb, mhppo_mlp mc, mhppo_mlp mw, mhppo_mlp md,
+                                                   int t, mhppo_eval_bufs E) {
+  extern __shared__ float lds[];
+  const int szc = mlp_size(NF_C, 1), dc = choice_dim(c), szd = mlp_size(dc, 2);
+  float *Wc = lds, *Ww = lds + szc, *Wd = lds + 2 * szc;
+  for (int i = threadIdx.x; i < szc; i += blockDim.x) {
+    Wc[i] = mc.packed[i];
+    Ww[i] = mw.packed[i];
+  }
+  for (int i = threadIdx.x; i < szd; i += blockDim.x) Wd[i] = md.packed[i];
+  __syncthreads();
+  const int e = blockIdx.x * TPB + threadIdx.x;
+  if (e >= c.N) return;
+  const ObsLayout L = obs_layout(c);
+  const int S = c.nS, P = c.P, N = c.N;
+  float *o = E.obs + (size_t)e * L.obs_dim;
+  int32_t *ad = E.a_d + (size_t)e * S * P;
+  double *epm = E.ep_min + (size_t)e * S;
+  if (t == 0 || E.trig[e]) {  // need_new_d (:175-188)
+    for (int i = 0; i < S; i++) epm[i] = 0.0;
+    for (int i = 0; i < S; i++)
+      for (int p = 0; p < P; p++) {
+        float fd[2 + 6 * (MAXS - 1) + 10], pr[2];
+        obs_car_ped_d(o, L, i, p, fd);
+        mlp_forward<0, 2>(Wd, dc, fd, pr);
+        float mx = pr[0] > pr[1] ? pr[0] : pr[1];
+        float e0 = expf(pr[0] - mx), e1 = expf(pr[1] - mx);
+        float sm = e0 + e1;
+        ad[i * P + p] = (e1 / sm > e0 / sm) ? 1 : 0;  // torch.argmax: first maximum
+      }
+  }
+  const size_t te = (size_t)t * N + e;
+  float *oh = E.obs_hist + te * L.obs_dim;
+  for (int k = 0; k < L.obs_dim; k++) oh[k] = o[k];
+  double act[2 * MAXS], rw[MAXS], rl[MAXS];
+  for (int i = 0; i < S; i++) {
+    double a = c.b10;  // np.array(car_b[1,0]) (:193)
+    for (int p = 0; p < P; p++) {
+      float f[NF_C];
+      obs_car_ped(o, L, i, p, f);
+      double cand;
+      if (f[7] != 0.0f) {  // left the lane: speed-limit tracking, clamped (:196-197)
+        double x = (10.0 - (double)f[0]) / c.dt;
+        double m = (c.b10 < x) ? c.b10 : x;
+        cand = (c.b00 > m) ? c.b00 : m;
+      } else {
+        const bool wait = (2 * ad[i * P + p] - 1) > 0;
+        float out;
+        mlp_forward<NF_C, 1>(wait ? Ww : Wc, NF_C, f, &out);
+        const mhppo_mlp &m = wait ? mw : mc;
+        float tt = tanhf(out) * m.std;
+        cand = (double)(tt + m.mean);
+      }
+      if (cand < a) a = cand;  // Python min keeps the first on ties (:205-206)
+      double lim = (10.0 - (double)f[0]) / c.dt;
+      if (lim < a) a = lim;
+    }
+    act[i] = a;
+    E.acts[te * S + i] = (float)a;
+  }
+  for (int i = 0; i < S; i++) act[S + i] = (double)(2 * ad[i] - 1);  // action_d_light: flat index (:188, :210)
+  const float prev1 = o[L.env_off + 1];
+  env_step_one<V>(c, eb, e, act, E.obs, rw, rl, E.saved + (size_t)t * N);  // writes done into saved[t][e]
+  const uint8_t done = E.saved[te];
+  for (int i = 0; i < S; i++) {
+    E.rews_c[te * S + i] = (float)rw[i];
+    double m = epm[i], x = rl[i];
+    epm[i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));  // np.minimum
+  }
+  const float cur1 = o[L.env_off + 1];
+  const uint8_t trig = L.scalable ? (cur1 != (float)P) : (cur1 != prev1);  // (:218-220)
+  const uint8_t saved = trig || done;
+  E.saved[te] = saved;
+  E.trig[e] = trig;
+  if (saved) {  // (:224-229)
+    for (int i = 0; i < S; i++) E.rews_d[te * S + i] = (float)epm[i];
+    for (int p = 0; p < P; p++) E.waiting[te * P + p] = (float)eb.ped[((size_t)P_WT * P + p) * N + e];
+  }
+}
+
 __global__ void __launch_bounds__(TPB) k_fill_f64(double *p, size_t n, double v) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i < n) p[i] = v;
@@ -404,6 +490,23 @@ int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo
   int rc = mhppo_rollout_policy(env, actor_cross, actor_wait, bufs, stream);
   if (rc) return rc;
   return mhppo_rollout_sample_env(env, eps, t, bufs, stream);
+}
+
+int mhppo_eval_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                    const mhppo_mlp *actor_choice, int t, mhppo_eval_bufs *bufs, void *stream) {
+  if (!env || !actor_cross || !actor_wait || !actor_choice || !bufs) return set_error(MHPPO_EINVAL, "null argument");
+  const Cfg &c = env_cfg(env);
+  if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
+    return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
+  if (actor_choice->n_in != choice_dim(c) || actor_choice->n_out != 2)
+    return set_error(MHPPO_EINVAL, "choice actor must be %d -> 2", choice_dim(c));
+  if (t < 0 || t >= bufs->T || t >= c.max_episode)
+    return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T < c.max_episode ? bufs->T : c.max_episode);
+  size_t shm = sizeof(float) * (2 * mlp_size(NF_C, 1) + mlp_size(choice_dim(c), 2));
+  VLAUNCH(k_eval_step, c.variant, grid_for(c.N), shm, (hipStream_t)stream, c, env_bufs(env), *actor_cross,
+          *actor_wait, *actor_choice, t, *bufs);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
 }
 
 int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream) {

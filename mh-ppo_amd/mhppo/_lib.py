@@ -36,6 +36,11 @@ class RolloutBufs(ctypes.Structure):
                 ("rew", P), ("ep_min", P), ("exist", P), ("T", I32), ("reserved", I32)]
 
 
+class EvalBufs(ctypes.Structure):
+    _fields_ = [("obs", P), ("a_d", P), ("trig", P), ("ep_min", P), ("obs_hist", P), ("acts", P), ("rews_c", P),
+                ("rews_d", P), ("waiting", P), ("saved", P), ("T", I32), ("reserved", I32)]
+
+
 # name: (restype, argtypes)
 _SIGS = {
     "mhppo_env_create": (I32, [ctypes.POINTER(EnvCfg), I32, ctypes.POINTER(P)]),
@@ -53,6 +58,8 @@ _SIGS = {
                                  ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_policy": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_eval_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), I32,
+                              ctypes.POINTER(EvalBufs), P]),
     "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
     "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),

@@ -38,11 +38,24 @@ class Env_rollout:
         self.shape_env_d = self.gpu.dc
         self.seed = 0
         self.iteration = 0
-        self.reset()
-
-    def reset(self):
+        self.env.reset(want_obs=False)  # the reference's __init__ resets the env (:107)
         self.batch = None
         self.cross = self.wait = self.choice = None
+
+    def reset(self):
+        """(:125-144) clears the batches and resets the env, consuming that reset's draws
+        in every env's random stream exactly as the reference does."""
+        self.env.reset(want_obs=False)
+        self.batch = None
+        self.cross = self.wait = self.choice = None
+
+    def iterations(self, actor_net_cross, actor_net_wait, actor_net_choice, nbr_episodes, choix=False):
+        """Deterministic evaluation (:152-252) of `nbr_episodes` consecutive episodes in every
+        env; returns (obs, acts, rews_c, rews_d, waiting_time) env-major (see RolloutGPU.evaluate)."""
+        if choix:
+            raise NotImplementedError("choix_test scripted scenario (:629-633) is not part of this build")
+        with torch.no_grad():
+            return self.gpu.evaluate(actor_net_cross, actor_net_wait, actor_net_choice, nbr_episodes)
 
     def iterations_rand(self, actor_net_cross, actor_net_wait, actor_net_choice, cov_mat=None, cov_mat_d=None,
                         batch_size=None, random_rate=0.0, forced_choice=None, eps_tape=None):
@@ -176,6 +189,13 @@ class Algo_PPO:
                                 float(b.item()) / (m_d if k == "choice" else (m_c if k == "cross" else m_w)))
                             for k, (a, b) in losses.items()} if self.verbose else losses
         return m_c, m_w, m_d
+
+    def evaluate(self, nbr_episodes, choix=False):
+        """(:738-747) rollout.reset() then the deterministic iterations; with N envs every env
+        plays `nbr_episodes` episodes (N * nbr_episodes in total, env-major)."""
+        self.rollout.reset()
+        return self.rollout.iterations(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
+                                       nbr_episodes, choix=choix)
 
     def train(self, nb_loop):
         """(:854-917)"""

@@ -63,6 +63,43 @@ class RolloutGPU:
         b.T = self.T
         self._bufs = b
 
+    def evaluate(self, actor_cross, actor_wait, actor_choice, episodes=1):
+        """Deterministic evaluation (Env_rollout.iterations :152-252): `episodes` consecutive
+        episodes in every env (env e's episodes continue its own random stream).
+        Returns the five tensors iterations returns, env-major (env 0's episodes first),
+        on the env's device: obs [N*K*T, obs_dim], acts [N*K*T, S], rews_c [N*K*T, S]
+        (float32), rews_d [saves, S], waiting [saves * P]."""
+        L = _lib.lib()
+        venv, N, S, P, T = self.venv, self.N, self.S, self.P, self.T
+        dev = venv.device
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
+        E = dict(obs=z((N, venv.obs_dim), torch.float32), a_d=z((N, S, P), torch.int32),
+                 trig=z(N, torch.uint8), ep_min=z((N, S), torch.float64))
+        hist = {k: [] for k in ("obs", "acts", "rews_c", "rews_d", "waiting", "saved")}
+        mc, tc = actor_cross.mlp_desc()
+        mw, tw = actor_wait.mlp_desc()
+        md, td = actor_choice.mlp_desc()
+        st = _lib.stream_ptr()
+        for _ in range(episodes):
+            R = dict(obs_hist=z((T, N, venv.obs_dim), torch.float32), acts=z((T, N, S), torch.float32),
+                     rews_c=z((T, N, S), torch.float32), rews_d=z((T, N, S), torch.float32),
+                     waiting=z((T, N, P), torch.float32), saved=z((T, N), torch.uint8))
+            b = _lib.EvalBufs()
+            for k, v in list(E.items()) + list(R.items()):
+                setattr(b, k, ctypes.c_void_p(v.data_ptr()))
+            b.T = T
+            _lib.check(L.mhppo_env_reset(venv.handle, _lib.ptr(E["obs"]), st))
+            for t in range(T):
+                _lib.check(L.mhppo_eval_step(venv.handle, ctypes.byref(mc), ctypes.byref(mw), ctypes.byref(md), t,
+                                             ctypes.byref(b), st))
+            hist["obs"].append(R["obs_hist"].transpose(0, 1))  # [N, T, od]
+            for k in ("acts", "rews_c", "rews_d", "waiting", "saved"):
+                hist[k].append(R[k].transpose(0, 1))
+        cat = {k: torch.stack(v, 1) for k, v in hist.items()}  # [N, K, T, ...]
+        saved = cat["saved"].reshape(-1).bool()
+        return (cat["obs"].reshape(-1, venv.obs_dim), cat["acts"].reshape(-1, S), cat["rews_c"].reshape(-1, S),
+                cat["rews_d"].reshape(-1, S)[saved], cat["waiting"].reshape(-1, P)[saved].reshape(-1))
+
     def draw_noise(self, seed, iteration):
         """Philox perf-mode noise for one iteration (global-env-id counters)."""
         L = _lib.lib()

@@ -157,6 +157,44 @@ def rollout(variant, nb_car, nb_ped, nb_lines, seeds, w_cross, w_wait, w_choice,
     return out
 
 
+def evaluate(variant, nb_car, nb_ped, nb_lines, seeds, episodes, w_cross, w_wait, w_choice, mean=-1.0, std=3.0,
+             acc_lo=-4.0, acc_hi=2.0, dt=0.3, T=80):
+    """Algo_PPO.evaluate (:738-747) restated: Env_rollout.reset() — which resets the env,
+    consuming that reset's draws (:125-129) — then Env_rollout.iterations (deterministic
+    evaluation): for each seed, `episodes` consecutive episodes on one env.  Returns a list (one per seed) of dicts shaped like
+    the five tensors iterations returns: obs [K*T, obs_dim], acts [K*T, S], rews_c
+    [K*T, S], rews_d [saves, S], waiting [saves * P]."""
+    L = lib()
+    P_ = ctypes.c_void_p
+    L.oracle_eval_episode.restype = ctypes.c_int
+    L.oracle_eval_episode.argtypes = [P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_, P_,
+                                      ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double] + [P_] * 6
+    S = 2 * nb_lines if variant == "scalable" else nb_car
+    wc, ww, wd = (np.ascontiguousarray(w, np.float32) for w in (w_cross, w_wait, w_choice))
+    res = []
+    for sd in seeds:
+        env = OracleEnv(variant, nb_car, nb_ped, nb_lines, seed=int(sd))
+        od = env.obs_dim
+        env.reset()  # Env_rollout.reset()
+        acc = {k: [] for k in ("obs", "acts", "rews_c", "rews_d", "waiting")}
+        for _ in range(episodes):
+            o = dict(obs=np.zeros((T, od), np.float32), acts=np.zeros((T, S), np.float32),
+                     rews_c=np.zeros((T, S), np.float32), saved=np.zeros(T, np.uint8),
+                     rews_d=np.zeros((T, S), np.float32), waiting=np.zeros((T, nb_ped), np.float32))
+            n = L.oracle_eval_episode(env.h, VARIANTS[variant], S, nb_ped, T, _p(wc), _p(ww), _p(wd), mean, std,
+                                      acc_lo, acc_hi, dt, *[_p(o[k]) for k in ("obs", "acts", "rews_c", "saved",
+                                                                             "rews_d", "waiting")])
+            sv = o["saved"][:n].astype(bool)
+            acc["obs"].append(o["obs"][:n])
+            acc["acts"].append(o["acts"][:n])
+            acc["rews_c"].append(o["rews_c"][:n])
+            acc["rews_d"].append(o["rews_d"][:n][sv])
+            acc["waiting"].append(o["waiting"][:n][sv].reshape(-1))
+        res.append({k: np.concatenate(v) for k, v in acc.items()})
+    return res
+
+
 _CPU_NETS = {}
 
 

@@ -16,6 +16,10 @@
  * the MVN standard normals come in as eps (recorded or Philox).
  * Model_PPO forward (:70-93): each output is a float32 fmaf chain over inputs in
  * ascending order from 0, plus bias, ReLU; tanh*std+mean; pairwise softmax.
+ *
+ * oracle_eval_episode restates one episode of the deterministic evaluation
+ * Env_rollout.iterations (Coop-MH-PPO-scalable.py:152-252; Coop-MH-PPO.ipynb /
+ * MH-PPO.ipynb same body), the routine Algo_PPO.evaluate (:738-747) runs.
  */
 #include <math.h>
 #include <stdint.h>
@@ -25,6 +29,7 @@ typedef struct OEnv OEnv;
 int oracle_env_obs_dim(const OEnv *e);
 void oracle_env_reset(OEnv *e, float *obs);
 int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards, double *reward_light);
+int oracle_env_dump(const OEnv *e, double *out);
 
 #define NF 13
 
@@ -237,6 +242,96 @@ int oracle_rollout_episode(OEnv *e, int variant, int S, int P, int T, const floa
             double m = o_ep_min[i], xx = rl[i];
             o_ep_min[i] = (m != m) ? m : ((xx != xx) ? xx : (xx < m ? xx : m));
         }
+        if (done) { t++; break; }
+    }
+    return t;
+}
+
+/* One episode of Env_rollout.iterations (:152-252), deterministic:
+ *  - at need_new_d (episode start; then whenever the re-decision test fires):
+ *    episodic_reward = 0, choice a_d[i*P+p] = argmax(actor_choice(obs_d)) (torch.argmax:
+ *    first maximum, :180-186)
+ *  - per car i: a = car_b[1,0]; per ped p (every ped, no exist gate): if obs_car_ped[7]
+ *    (the pedestrian has left the car's lane): cand = max(min((10 - V)/dt, car_b[1,0]),
+ *    car_b[0,0]) else the cross (action_d <= 0) / wait actor's mean output; a =
+ *    min(a, cand); a = min(a, (10 - V)/dt) — Python min keeps the first on ties (:193-207)
+ *  - lights: action_d_light = 2*action_all_d - 1, i.e. entry i of the FLAT (car, ped)
+ *    choice array, not the closest pedestrian's (:188, :210; the env reads entries S..2S-1)
+ *  - env.step; rews_c = reward; episodic_reward = np.minimum(.., reward_light) (:212-216)
+ *  - re-decision test (:218-220): scalable driver state["env"][1] != nb_ped; coop and
+ *    naif drivers state["env"][1] != its previous value; a save (rews_d = episodic_reward,
+ *    every pedestrian's waiting_time) happens when it fires or at done (:224-229).
+ * Outputs per step t: obs (the pre-step observation), acts [S] and rews_c [S] as
+ * float32 (torch.tensor(..., dtype=float)), saved flag, rews_d [S] and waiting [P]
+ * when saved.  Returns the number of steps played. */
+int oracle_eval_episode(OEnv *e, int variant, int S, int P, int T, const float *w_cross, const float *w_wait,
+                        const float *w_choice, float act_mean, float act_std, double acc_lo, double acc_hi,
+                        double dt, float *o_obs, float *o_acts, float *o_rews_c, uint8_t *o_saved, float *o_rews_d,
+                        float *o_waiting) {
+    Lay L = layout(variant, S, P);
+    const int dc = oracle_choice_dim(variant, S), od = oracle_env_obs_dim(e);
+    float obs[1024];
+    double actions[64], rew[32], rl[32], epr[32], dump[4096];
+    int a_d[256];
+    oracle_env_reset(e, obs);
+    int need = 1, t;
+    for (t = 0; t < T; t++) {
+        if (need) {
+            for (int i = 0; i < S; i++) epr[i] = 0.0;
+            for (int i = 0; i < S; i++)
+                for (int p = 0; p < P; p++) {
+                    float f[256], lg[2];
+                    feat_d(obs, &L, i, p, f);
+                    oracle_mlp_forward(w_choice, dc, 2, f, lg);
+                    float mx = lg[0] > lg[1] ? lg[0] : lg[1];
+                    float e0 = expf(lg[0] - mx), e1 = expf(lg[1] - mx);
+                    float sm = e0 + e1;
+                    a_d[i * P + p] = (e1 / sm > e0 / sm) ? 1 : 0;
+                }
+        }
+        need = 0;
+        memcpy(o_obs + (size_t)t * od, obs, sizeof(float) * od);
+        for (int i = 0; i < S; i++) {
+            double a = acc_hi;
+            for (int p = 0; p < P; p++) {
+                float f[NF];
+                feat_c(obs, &L, i, p, f);
+                double cand;
+                if (f[7] != 0.0f) {
+                    double x = (10.0 - (double)f[0]) / dt;
+                    double m = (acc_hi < x) ? acc_hi : x;
+                    cand = (acc_lo > m) ? acc_lo : m;
+                } else {
+                    int wait = (2 * a_d[i * P + p] - 1) > 0;
+                    float out;
+                    oracle_mlp_forward(wait ? w_wait : w_cross, NF, 1, f, &out);
+                    float tt = tanhf(out) * act_std;
+                    cand = (double)(tt + act_mean);
+                }
+                if (cand < a) a = cand;
+                double lim = (10.0 - (double)f[0]) / dt;
+                if (lim < a) a = lim;
+            }
+            actions[i] = a;
+            o_acts[(size_t)t * S + i] = (float)a;
+        }
+        for (int i = 0; i < S; i++) actions[S + i] = (double)(2 * a_d[i] - 1);
+        const float prev1 = obs[L.env_off + 1];
+        int done = oracle_env_step(e, actions, obs, rew, rl);
+        for (int i = 0; i < S; i++) {
+            o_rews_c[(size_t)t * S + i] = (float)rew[i];
+            double m = epr[i], x = rl[i];
+            epr[i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));
+        }
+        const float cur1 = obs[L.env_off + 1];
+        int trig = L.scalable ? (cur1 != (float)P) : (cur1 != prev1);
+        o_saved[t] = (uint8_t)(trig || done);
+        if (o_saved[t]) {
+            oracle_env_dump(e, dump);
+            for (int i = 0; i < S; i++) o_rews_d[(size_t)t * S + i] = (float)epr[i];
+            for (int p = 0; p < P; p++) o_waiting[(size_t)t * P + p] = (float)dump[20 * p + 12];
+        }
+        if (trig) need = 1;
         if (done) { t++; break; }
     }
     return t;
