@@ -59,6 +59,15 @@ void mhppo_env_destroy(mhppo_env *env);
 int mhppo_env_obs_dim(const mhppo_env *env);
 int mhppo_env_slots(const mhppo_env *env);   /* S: AV action slots per env */
 
+/* Checkpoint/resume (the reference saves only weights, :985-1001):
+ * the env's whole device state — every field of every env plus its CPython MT19937
+ * stream (624 words + cursor) — as one opaque blob of mhppo_env_state_bytes bytes.
+ * export copies it to `dst`, import restores it from `src` (host or device memory,
+ * stream-ordered); a blob is valid only for a handle created with the same config. */
+int64_t mhppo_env_state_bytes(const mhppo_env *env);
+int mhppo_env_export(const mhppo_env *env, void *dst, void *stream);
+int mhppo_env_import(mhppo_env *env, const void *src, void *stream);
+
 /* Replaces Crosswalk_*.reset() (Env_hybrid_multi_coop.py:838-893; 4cars :850-911;
  * scalable :884-946).  obs: float32 [N, obs_dim] or NULL. */
 int mhppo_env_reset(mhppo_env *env, float *obs, void *stream);

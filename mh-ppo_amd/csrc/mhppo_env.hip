@@ -57,6 +57,7 @@ struct mhppo_env {
   Bufs b;
   int device;
   void *blob;
+  size_t blob_bytes;
 };
 
 #define VARIANT_LAUNCH(kern, variant, grid, stream, ...)                                    \
@@ -99,6 +100,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
     delete h;
     return set_error(MHPPO_ENOMEM, "hipMalloc(%zu) failed", total);
   }
+  h->blob_bytes = total;
   char *p = (char *)h->blob;
   h->b.car = (double *)p; p += al(bytes_car);
   h->b.ped = (double *)p; p += al(bytes_ped);
@@ -125,6 +127,20 @@ void mhppo_env_destroy(mhppo_env *env) {
 int mhppo_env_obs_dim(const mhppo_env *env) { return env ? env->c.obs_dim : MHPPO_EINVAL; }
 int mhppo_env_slots(const mhppo_env *env) { return env ? env->c.nS : MHPPO_EINVAL; }
 int mhppo_env_state_dim(const mhppo_env *env) { return env ? 21 * env->c.P + 8 * env->c.nC + 4 : MHPPO_EINVAL; }
+
+int64_t mhppo_env_state_bytes(const mhppo_env *env) { return env ? (int64_t)env->blob_bytes : MHPPO_EINVAL; }
+
+int mhppo_env_export(const mhppo_env *env, void *dst, void *stream) {
+  if (!env || !dst) return set_error(MHPPO_EINVAL, "null argument");
+  CHECK_HIP(hipMemcpyAsync(dst, env->blob, env->blob_bytes, hipMemcpyDefault, (hipStream_t)stream));
+  return MHPPO_OK;
+}
+
+int mhppo_env_import(mhppo_env *env, const void *src, void *stream) {
+  if (!env || !src) return set_error(MHPPO_EINVAL, "null argument");
+  CHECK_HIP(hipMemcpyAsync(env->blob, src, env->blob_bytes, hipMemcpyDefault, (hipStream_t)stream));
+  return MHPPO_OK;
+}
 
 int mhppo_env_reset(mhppo_env *env, float *obs, void *stream) {
   if (!env) return set_error(MHPPO_EINVAL, "null env");

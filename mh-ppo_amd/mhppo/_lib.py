@@ -49,6 +49,9 @@ _SIGS = {
     "mhppo_env_slots": (I32, [P]),
     "mhppo_env_state_dim": (I32, [P]),
     "mhppo_env_reset": (I32, [P, P, P]),
+    "mhppo_env_state_bytes": (I64, [P]),
+    "mhppo_env_export": (I32, [P, P, P]),
+    "mhppo_env_import": (I32, [P, P, P]),
     "mhppo_env_step": (I32, [P, P, P, P, P, P, P]),
     "mhppo_env_get_state": (I32, [P, P, P]),
     "mhppo_env_get_rng": (I32, [P, P, P, P]),

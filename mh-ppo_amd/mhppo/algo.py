@@ -21,6 +21,16 @@ from .rollout import RolloutGPU, bucket_segments
 PREFIX = {"scalable": "pappo-scalable-coop", "coop": "pappo-coop", "4cars": "pappo-coop-4cars", "naif": "pappo-acc6"}
 
 
+def _rank():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def _rank_path(path):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return f"{path}.rank{dist.get_rank()}"
+    return path
+
+
 def _venv(env):
     return env.venv if hasattr(env, "venv") else env
 
@@ -198,31 +208,52 @@ class Algo_PPO:
                                        nbr_episodes, choix=choix)
 
     def train(self, nb_loop):
-        """(:854-917)"""
+        """(:854-917): per iteration rollout.reset() -> one episode per env -> 10 + 10 epochs
+        -> reward curves -> rollout.reset() (both resets consume env draws, as in the
+        reference); at the end the curves go to load_model/parameters/*.npy (:908-916)."""
         for ep in range(nb_loop):
             self.rollout.reset()
             self.rollout.iterations_rand(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
                                          self.cov_mat, self.cov_mat_d, self.batch_size)
             m_c, m_w, m_d = self.update()
-            if self.verbose:
-                rc, rw, rd = self.rollout.immediate_rewards()
-                dev = self.venv.device
-                sums = torch.tensor([float(rc.sum()), float(rw.sum()), float(rd.sum())], dtype=torch.float64,
-                                    device=dev)
-                ppo._allreduce_(sums)
-                if m_c > 0:
-                    self.ep_reward_cross.append(float(sums[0]) / (m_c))
-                if m_w > 0:
-                    self.ep_reward_wait.append(float(sums[1]) / (m_w))
-                self.ep_reward_choice.append(float(sums[2]) / max(m_d, 1))
-                self.ep_scenario_balance.append([int(m_c), int(m_w)])
+            rc, rw, rd = self.rollout.immediate_rewards()
+            dev = self.venv.device
+            sums = torch.stack([rc.double().sum(), rw.double().sum(), rd.double().sum()]).to(dev)
+            ppo._allreduce_(sums)
+            sums = sums.tolist()
+            if m_c > 0:  # rew_batch.mean() over the global batch (:886-892)
+                self.ep_reward_cross.append(sums[0] / m_c)
+            if m_w > 0:
+                self.ep_reward_wait.append(sums[1] / m_w)
+            self.ep_reward_choice.append(sums[2] / max(m_d, 1))
+            self.ep_scenario_balance.append([int(m_c), int(m_w)])
+            if self.verbose and _rank() == 0:
                 print("Episode * {} * And Number of steps is ==> {}".format(ep, ep * self.batch_size))
                 print("Average Cross reward is ==> {}, Average Wait reward is ==> {}".format(
                     np.mean(self.ep_reward_cross[-10:]) if self.ep_reward_cross else float("nan"),
                     np.mean(self.ep_reward_wait[-10:]) if self.ep_reward_wait else float("nan")))
                 print("Average Choice reward is ==> {}".format(np.mean(self.ep_reward_choice[-10:])))
                 print("Number Cross is ==> {} and Number Wait is ==> {} ".format(int(m_c), int(m_w)))
+            self.rollout.reset()
             self.total_loop = self.total_loop + 1
+        if _rank() == 0:
+            self.save_reward_curves()
+        if self.verbose and _rank() == 0:
+            print("Complete")
+
+    def _curve_path(self, name):
+        pre = PREFIX.get(self.venv.variant, "pappo")
+        return "load_model/parameters/{}-{:02d}-{}-step-{:03d}000.npy".format(pre, self.num_algo, name,
+                                                                             int(self.total_loop / 1000))
+
+    def save_reward_curves(self):
+        """(:908-916) reward_cross / reward_wait / reward_choice / scenario_balance."""
+        os.makedirs("load_model/parameters", exist_ok=True)
+        for name, v in (("reward_cross", np.array(self.ep_reward_cross)), ("reward_wait", np.array(self.ep_reward_wait)),
+                        ("reward_choice", np.array(self.ep_reward_choice)),
+                        ("scenario_balance", np.array(self.ep_scenario_balance).reshape((-1, 2)))):
+            with open(self._curve_path(name), "wb") as f:
+                np.save(f, v)
 
     # --------------------------------------------------------------- checkpoints
     def _path(self, head, kind, num_algo, total_loop):
@@ -239,6 +270,55 @@ class Algo_PPO:
                 sd = torch.load(self._path(head, kind, num_algo, total_loop), map_location=self.venv.device,
                                 weights_only=True)
                 net.load_state_dict(sd)
+
+    def loading_curriculum(self, num_actor, num_algo, total_loop):
+        """(:957-983) load one head's actor + critic: 0 cross, 1 wait, 2 choice."""
+        self.total_loop = total_loop
+        head = ("cross", "wait", "choice")[num_actor]
+        for kind in ("actor", "critic"):
+            net = getattr(self, f"{kind}_net_{head}")
+            net.load_state_dict(torch.load(self._path(head, kind, num_algo, total_loop),
+                                           map_location=self.venv.device, weights_only=True))
+
+    # Checkpoint/resume beyond the reference (SURVEY §8(f)2): the reference keeps only
+    # weights; an exact resume also needs the Adam moments, every env's state and random
+    # stream, the rollout noise counter and the reward curves.
+    def _optimizers(self):
+        return {f"{k}_{h}": getattr(self, f"optimizer_{k}_{h}") for h in ("cross", "wait", "choice")
+                for k in ("actor", "critic")}
+
+    def save_checkpoint(self, path):
+        """Everything needed to continue training bit-identically.  Under data parallelism
+        every rank writes `path.rank<r>` (its env shard differs; nets/Adam are replicated)."""
+        ck = {
+            "nets": {f"{k}_{h}": getattr(self, f"{k}_net_{h}").state_dict() for h in ("cross", "wait", "choice")
+                     for k in ("actor", "critic")},
+            "optim": {k: o.state_dict() for k, o in self._optimizers().items()},
+            "env": self.venv.state_dict(),
+            "rollout": {"iteration": int(self.rollout.iteration), "seed": int(self.rollout.seed)},
+            "algo": {"num_algo": int(self.num_algo), "total_loop": int(self.total_loop)},
+            "curves": {"cross": [float(x) for x in self.ep_reward_cross],
+                       "wait": [float(x) for x in self.ep_reward_wait],
+                       "choice": [float(x) for x in self.ep_reward_choice],
+                       "balance": [[int(a), int(b)] for a, b in self.ep_scenario_balance]},
+        }
+        torch.save(ck, _rank_path(path))
+
+    def load_checkpoint(self, path):
+        """Inverse of save_checkpoint (weights_only load: tensors and plain containers only)."""
+        ck = torch.load(_rank_path(path), map_location="cpu", weights_only=True)
+        for name, sd in ck["nets"].items():
+            k, h = name.split("_")
+            getattr(self, f"{k}_net_{h}").load_state_dict(sd)
+        for name, o in self._optimizers().items():
+            o.load_state_dict(ck["optim"][name])
+        self.venv.load_state_dict(ck["env"])
+        self.rollout.iteration = ck["rollout"]["iteration"]
+        self.rollout.seed = ck["rollout"]["seed"]
+        self.num_algo, self.total_loop = ck["algo"]["num_algo"], ck["algo"]["total_loop"]
+        c = ck["curves"]
+        self.ep_reward_cross, self.ep_reward_wait = list(c["cross"]), list(c["wait"])
+        self.ep_reward_choice, self.ep_scenario_balance = list(c["choice"]), [list(x) for x in c["balance"]]
 
     def saving(self):
         """(:985-1001)"""

@@ -115,3 +115,28 @@ class VecCrosswalk:
         mti = self._t((self.n_envs,), torch.int32)
         _lib.check(_lib.lib().mhppo_env_get_rng(self._h, _lib.ptr(mt), _lib.ptr(mti), _lib.stream_ptr()))
         return mt, mti
+
+    # ------------------------------------------------------------ checkpoint
+    def _cfg_key(self):
+        c = self.cfg
+        return [int(c.variant), int(c.n_envs), int(c.nb_car), int(c.nb_ped), int(c.nb_lines), int(c.max_episode),
+                int(c.sin_model), float(c.dt), [float(x) for x in c.car_b], [float(x) for x in c.ped_b],
+                [float(x) for x in c.cross_b], int(c.seed_base), int(c.env_id_offset)]
+
+    def state_dict(self):
+        """Whole device state (all env fields + every env's MT19937 stream), for exact resume."""
+        L = _lib.lib()
+        n = int(L.mhppo_env_state_bytes(self._h))
+        blob = torch.empty(n, dtype=torch.uint8, device=self.device)
+        _lib.check(L.mhppo_env_export(self._h, _lib.ptr(blob), _lib.stream_ptr()))
+        return {"cfg": self._cfg_key(), "blob": blob.cpu()}
+
+    def load_state_dict(self, sd):
+        if list(sd["cfg"]) != self._cfg_key():
+            raise ValueError("env checkpoint was made for another configuration")
+        L = _lib.lib()
+        blob = sd["blob"].to(device=self.device, dtype=torch.uint8).contiguous()
+        if blob.numel() != int(L.mhppo_env_state_bytes(self._h)):
+            raise ValueError("env checkpoint size mismatch")
+        _lib.check(L.mhppo_env_import(self._h, _lib.ptr(blob), _lib.stream_ptr()))
+        torch.cuda.current_stream(self.device).synchronize()

@@ -1,0 +1,33 @@
+"""Checkpoint / reward-curve file names and keys follow the reference's formats
+(Algo_PPO.loading/saving :935-1001, reward curves :908-916) and its shipped files."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mh-ppo_amd")]
+
+
+class _V:
+    variant = "scalable"
+
+
+def _algo(num_algo, total_loop):
+    from mhppo.algo import Algo_PPO
+    a = Algo_PPO.__new__(Algo_PPO)
+    a.venv, a.num_algo, a.total_loop = _V(), num_algo, total_loop
+    return a
+
+
+def test_weight_paths_match_reference_format():
+    a = _algo(111, 1000)
+    ref = "load_model/weights/pappo-scalable-coop-cross-{num_algo:02d}-actor-step-{epoch:03d}0.pth"
+    assert a._path("cross", "actor", 111, 1000) == ref.format(num_algo=111, epoch=100)
+    # the shipped checkpoint names (load_model/weights/*.pth) come out of the same format
+    assert os.path.basename(a._path("choice", "critic", 111, 1000)) == "pappo-scalable-coop-choice-111-critic-step-1000.pth"
+
+
+def test_reward_curve_paths_match_reference_format():
+    a = _algo(111, 1000)
+    ref = "load_model/parameters/pappo-scalable-coop-{num_algo:02d}-{name}-step-{epoch:03d}000.npy"
+    for name in ("reward_cross", "reward_wait", "reward_choice", "scenario_balance"):
+        assert a._curve_path(name) == ref.format(num_algo=111, epoch=1, name=name)
