@@ -31,6 +31,9 @@ extern "C" {
 #define MHPPO_4CARS 1     /* Crosswalk_hybrid_multi_coop_4cars-v0    Env_hybrid_multi_coop_4cars.py:667 */
 #define MHPPO_SCALABLE 2  /* Crosswalk_hybrid_multi_coop_scalable-v0 Env_hybrid_multi_coop_scalable.py:668 */
 #define MHPPO_NAIF 3      /* Crosswalk_hybrid_multi_naif-v0          Env_hybrid_multi_naif.py:616 */
+#define MHPPO_4CARS2 4    /* Crosswalk_hybrid_multi_coop_4cars2-v0   Env_hybrid_multi_coop_4cars2.py:683
+                             (env only: actions [AV acc, follower acc, AV light, follower light]) */
+#define MHPPO_STOP 5      /* Crosswalk_hybrid_multi_stop-v0          Env_hybrid_multi_stop.py:634 */
 
 typedef struct mhppo_env_cfg {
     int32_t variant;      /* MHPPO_* */
@@ -57,7 +60,9 @@ void mhppo_env_destroy(mhppo_env *env);
 
 /* Geometry of the flat observation (gym-sorted keys car|car_follow|env|ped) and slots. */
 int mhppo_env_obs_dim(const mhppo_env *env);
-int mhppo_env_slots(const mhppo_env *env);   /* S: AV action slots per env */
+int mhppo_env_slots(const mhppo_env *env);   /* S: action slots per env (actions are [N, 2S]) */
+int mhppo_env_reward_slots(const mhppo_env *env); /* reward/reward_light width: S, except 4cars2 = nb_car
+                                                     (its PPO-driven followers earn none, :836-847) */
 
 /* Checkpoint/resume (the reference saves only weights, :985-1001):
  * the env's whole device state — every field of every env plus its CPython MT19937

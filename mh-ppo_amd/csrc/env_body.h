@@ -32,7 +32,7 @@ MHPPO_HD void ped_init(Env<V> &E, Ped &q, int is_crossing, int exist) {
   if (!exist) {
     q.ivx = 0.;
     q.ivy = 0.;
-    if (V == V_4CARS || V == V_NAIF) px = c.pb[0][2];
+    if (V == V_4CARS || V == V_NAIF || V == V_4CARS2 || V == V_STOP) px = c.pb[0][2];
     py = c.pb[0][3] * (double)q.dir;
   } else if (!is_crossing) {
     q.ivx = 0.;
@@ -56,7 +56,7 @@ MHPPO_HD void ped_init(Env<V> &E, Ped &q, int is_crossing, int exist) {
   if (V == V_COOP) {
     q.set(F_NEEDSTOP, true);
     q.cstop = r.uniform(-E.cl / 2 + 0.2, E.cl / 2 - 0.2);
-  } else if (V == V_SCALABLE) {
+  } else if (V == V_SCALABLE || V == V_4CARS2 || V == V_STOP) {
     q.set(F_NEEDSTOP, r.uniform(0, 1) < 0.5);
     q.cstop = r.uniform(-E.cl / 2 + 0.2, E.cl / 2 - 0.2);
   }
@@ -171,8 +171,8 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
     }
   } else {
     for (int i = 0; i < c.nb_car; i++) car_init(E, i, (double)(i % c.nb_lines), 0, 1);
-    if (V == V_4CARS)
-      for (int i = 0; i < c.nb_car; i++) car_init(E, c.nS + i, E.car(C_LINE, i), 0, 1);
+    if (has_followers(V))
+      for (int i = 0; i < c.nb_car; i++) car_init(E, c.nAV + i, E.car(C_LINE, i), 0, 1);
   }
   b.envi[EI_CARTRAF * c.N + e] = car_traffic;
   int ped_traffic = E.rng.randint(1, c.nb_ped);
@@ -182,12 +182,13 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
     ped_init(E, q, 1, 1);
     store_ped(E, p, q, false);
   }
-  if (V == V_4CARS) {
-    for (int i = 0; i < c.nb_car; i++) {  // reset_car(speed_limit, Sc - 15., 0, line) (:878-879)
-      E.car(C_SC, c.nS + i) = E.car(C_SC, i) - 15.;
-      E.car(C_VC, c.nS + i) = 10.0;
-      E.car(C_LIGHT, c.nS + i) = 0.;
-      E.car(C_LINE, c.nS + i) = E.car(C_LINE, i);
+  if (has_followers(V)) {
+    for (int i = 0; i < c.nb_car; i++) {  // reset_car(speed_limit, Sc - 15., 0, line) (:878-879; 4cars2 Sc - U(10,30) :895)
+      const double gap = V == V_4CARS2 ? E.rng.uniform(10, 30) : 15.;
+      E.car(C_SC, c.nAV + i) = E.car(C_SC, i) - gap;
+      E.car(C_VC, c.nAV + i) = 10.0;
+      E.car(C_LIGHT, c.nAV + i) = 0.;
+      E.car(C_LINE, c.nAV + i) = E.car(C_LINE, i);
     }
   }
   env_observe(E, 0, obs);
@@ -196,12 +197,12 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
 }
 
 // ------------------------------------------------------------------ step
-// act: this env's [2S] actions; rw/rl: this env's [S] outputs (nullable)
+// act: this env's [2 nS] actions [acc..., light...]; rw/rl: this env's [nAV] outputs (nullable)
 template <int V>
 MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act, float *obs, double *rw,
                            double *rl, uint8_t *done) {
   Env<V> E(c, b, e);
-  const int nS = c.nS;
+  const int nS = c.nAV;  // AV slots (4cars2: followers handled below)
   double time = b.envd[E_TIME * c.N + e];
   double prev[MAXS];
   for (int i = 0; i < nS; i++) prev[i] = E.car(C_SC, i);
@@ -213,12 +214,17 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
         idm = car_follow_action(E, i, E.car(C_VC, i - 1), E.car(C_SC, i - 1));
       a = pymin(idm, a);
     }
-    car_step(E, i, a, act[i + nS]);
+    car_step(E, i, a, act[i + c.nS]);
   }
-  if (V == V_4CARS)
+  if (has_followers(V))
     for (int i = 0; i < c.nb_car; i++) {
       double a = car_follow_action(E, nS + i, E.car(C_VC, i), E.car(C_SC, i));
-      car_step(E, nS + i, a, E.car(C_LIGHT, i));
+      double light = E.car(C_LIGHT, i);
+      if (V == V_4CARS2) {  // follower step(action_ppo, action_light, leader) (:75-79, :811)
+        a = pymin(a, act[nS + i]);
+        light = act[c.nS + nS + i];
+      }
+      car_step(E, nS + i, a, light);
     }
   for (int p = 0; p < c.P; p++) {
     Ped q = load_ped(E, p);
@@ -300,7 +306,7 @@ MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int
 // config are evaluated here, with glibc, exactly as the reference does)
 inline void build_cfg(const mhppo_env_cfg &cfg_, Cfg &c) {
   const mhppo_env_cfg *cfg = &cfg_;
-  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : cfg->nb_car;
+  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : (cfg->variant == V_4CARS2 ? 2 : 1) * cfg->nb_car;
   memset(&c, 0, sizeof(c));
   c.variant = cfg->variant;
   c.N = cfg->n_envs;
@@ -308,11 +314,12 @@ inline void build_cfg(const mhppo_env_cfg &cfg_, Cfg &c) {
   c.nb_ped = cfg->nb_ped;
   c.nb_lines = cfg->nb_lines;
   c.nS = nS;
-  c.nC = cfg->variant == V_4CARS ? 2 * nS : nS;
+  c.nAV = cfg->variant == V_4CARS2 ? cfg->nb_car : nS;
+  c.nC = has_followers(cfg->variant) ? 2 * cfg->nb_car : nS;
   c.P = cfg->nb_ped;
   c.max_episode = cfg->max_episode;
   c.sin_model = cfg->sin_model;
-  c.obs_dim = cfg->variant == V_4CARS ? 12 * nS + 3 + 9 * c.P
+  c.obs_dim = has_followers(cfg->variant) ? 12 * cfg->nb_car + 3 + 9 * c.P
                                       : (cfg->variant == V_SCALABLE ? 7 * nS + 4 + 9 * c.P : 6 * nS + 3 + 9 * c.P);
   c.dt = cfg->dt;
   c.dt2 = pow(cfg->dt, 2.0);  // math.pow(self.dt, 2.0) (:604), glibc on the host

@@ -29,7 +29,9 @@
 
 namespace mhppo {
 
-enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3 };
+enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP = 5 };
+// 4cars / 4cars2: nb_car AVs, each followed by an IDM car (4cars2: PPO-driven follower)
+constexpr bool has_followers(int v) { return v == V_4CARS || v == V_4CARS2; }
 
 // car fields (double) [C_NF][nC][N]
 enum { C_AC, C_VC, C_SC, C_LIGHT, C_PA, C_ES, C_TS, C_H0, C_H1, C_LINE, C_EXIST, C_NF };
@@ -50,7 +52,9 @@ enum { E_CROSS, E_TIME, E_ND };
 enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_NI };
 
 struct Cfg {
-  int variant, N, nb_car, nb_ped, nb_lines, nS, nC, P, max_episode, sin_model, obs_dim, pad;
+  // nS: action slots (acc + light each); nAV: AV slots with rewards/detection (= nS except
+  // 4cars2, whose followers take actions but earn none); nC: all car slots (+ followers)
+  int variant, N, nb_car, nb_ped, nb_lines, nS, nC, P, max_episode, sin_model, obs_dim, nAV;
   double dt, dt2, b00, b10, pb[2][4], xb0, xb1, idm_den, ep_len;
   // car.__init__ position bounds (:549-560): low/high_car_range, mean_speed_ped (host-computed)
   double car_low, car_high, mean_speed_ped;
@@ -249,7 +253,7 @@ MHPPO_HD inline bool is_crossing_in_front(const Env<V> &E, const Ped &q, double 
 // mode 1 = step (existing AVs [+ followers for 4cars])
 template <int V>
 MHPPO_HD inline bool in_view(const Env<V> &E, int s, int mode) {
-  if (V == V_4CARS) return mode == 1 || s < E.c.nS;
+  if (has_followers(V)) return mode == 1 || s < E.c.nAV;
   if (V == V_SCALABLE) return mode == 0 || E.car(C_EXIST, s) != 0.0;
   return true;
 }
@@ -298,7 +302,7 @@ MHPPO_HD inline bool choix_pedestrian(Env<V> &E, const Ped &q, int mode) {
         if (E.car(C_SC, i) < q.Sx && E.car(C_LIGHT, i) < 0) return false;
       }
     } else {
-      if (V != V_4CARS && n > 1)
+      if (!has_followers(V) && n > 1)
         for (int i = n - 1; i >= 1; i--) (void)E.rng.randbelow((uint32_t)(i + 1));
       for (int s = 0; s < E.c.nC; s++) {
         if (!in_view(E, s, mode)) continue;
@@ -372,7 +376,7 @@ template <int V>
 MHPPO_HD inline double new_reward_wait_safety(const Env<V> &E, Ped &q, double spd, double pos, double line) {
   if ((!q.has(F_LEFT)) && q.has(F_ISCROSS) && (pos < q.Sx) && is_in_front(E, q, line, 0)) {
     double exp_dl;
-    if (spd < 0.05) {
+    if (spd < (V == V_STOP ? 0.01 : 0.05)) {  // stop :478
       exp_dl = 0.;
     } else {
       double dl = delta_l(E, q, pos, spd, line) / (spd);
@@ -461,8 +465,9 @@ MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
         q.Vy = 0.0;
         q.t0 = q.t0 + dt;
         if (change_line) q.wt = q.wt + dt;
-      } else if (V == V_SCALABLE && q.has(F_NEEDSTOP) && q.Sy < q.cstop && pp_y > q.cstop) {
-        q.tstop = E.rng.randint(5, 35);
+      } else if ((V == V_SCALABLE || V == V_4CARS2 || V == V_STOP) && q.has(F_NEEDSTOP) && q.Sy < q.cstop &&
+                 pp_y > q.cstop) {  // mid-crossing stop (scalable :371-381, 4cars2 :448, stop :366)
+        q.tstop = V == V_STOP ? E.rng.randint(2, 15) : E.rng.randint(5, 35);
         q.set(F_NEEDSTOP, false);
         if (!choose) {
           q.set(F_DECISION, false);
@@ -497,7 +502,7 @@ MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
         q.Sy = dir * ((cl - dtc) - cl / 2.);
       }
     } else {
-      q.tstop = E.rng.randint(2, 5);
+      q.tstop = V == V_4CARS2 ? E.rng.randint(5, 35) : (V == V_STOP ? E.rng.randint(2, 15) : E.rng.randint(2, 5));
       if (!choose) {
         q.set(F_DECISION, false);
         q.tstop = 0;
@@ -520,7 +525,7 @@ MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
 // accumulates this ped's per-slot danger into acc[] (caller passes registers)
 template <int V, int MAXS>
 MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double *acc, bool add) {
-  const int nS = E.c.nS;
+  const int nS = E.c.nAV;  // detection runs over the AVs (followers excluded, :845)
   for (int i = 0; i < nS; i++) {
     bool cond = is_in_front(E, q, E.car(C_LINE, i), 0);
     if (V == V_SCALABLE) cond = cond && (E.car(C_EXIST, i) != 0.0);
@@ -542,7 +547,7 @@ MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double
       else dl = worst_delta_l(E, q, Sc, Vc, line) / (Vc);
       double pa;
       if (dl > 0) pa = -1. * exp(-4. * (dl));
-      else pa = (V == V_NAIF) ? -1. * dl - 1 : 1. * dl - 1;
+      else pa = (V == V_NAIF || V == V_STOP) ? -1. * dl - 1 : 1. * dl - 1;
       E.car(C_PA, i) = pymin(E.car(C_PA, i), pa);
     }
     double Ts = E.car(C_TS, i);
@@ -574,7 +579,7 @@ MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double
   for (int i = 0; i < nS && i < MAXS; i++) {
     double res = E.car(C_PA, i) + E.car(C_ES, i);
     double term = 0.5 * green * (double)(E.car(C_LIGHT, i) < 0.) * (double)(E.car(C_TS, i) > 0);
-    if (V == V_COOP) res = res + term;
+    if (V == V_COOP || V == V_4CARS2 || V == V_STOP) res = res + term;
     else if (V == V_4CARS || V == V_SCALABLE) res = res - term;
     if (V == V_SCALABLE && E.car(C_EXIST, i) == 0.0) res = 0.;
     acc[i] += res;
@@ -600,6 +605,7 @@ MHPPO_HD inline void car_step(const Env<V> &E, int s, double action, double ligh
   if (Vc == 0.) sg = pymax(0., acc / fabs(acc));
   else if (acc > 0) sg = 1;
   else sg = pymax(pymin(-Vc / (dt * acc), 1.), 0.);
+  if (V == V_STOP && sg > 0.) acc = pymax(acc, -Vc / (dt * sg));  // stop :603-605
   double h0 = E.car(C_H0, s), h1 = E.car(C_H1, s);
   double fa = 0.0;
   fa = fa + 1.0 * acc;

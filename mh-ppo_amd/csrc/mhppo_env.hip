@@ -29,8 +29,8 @@ __global__ void __launch_bounds__(TPB)
     k_env_step(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
   int e = blockIdx.x * TPB + threadIdx.x;
   if (e < c.N)
-    env_step_one<V>(c, b, e, actions + (size_t)e * 2 * c.nS, obs, rew ? rew + (size_t)e * c.nS : nullptr,
-                    rlight ? rlight + (size_t)e * c.nS : nullptr, done);
+    env_step_one<V>(c, b, e, actions + (size_t)e * 2 * c.nS, obs, rew ? rew + (size_t)e * c.nAV : nullptr,
+                    rlight ? rlight + (size_t)e * c.nAV : nullptr, done);
 }
 
 __global__ void __launch_bounds__(TPB) k_env_seed(Cfg c, Bufs b) {
@@ -66,7 +66,9 @@ struct mhppo_env {
       case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;   \
       case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break; \
       case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break; \
-      default: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;       \
+      case V_NAIF: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;      \
+      case V_4CARS2: hipLaunchKernelGGL(kern<V_4CARS2>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;  \
+      default: hipLaunchKernelGGL(kern<V_STOP>, grid, dim3(TPB), 0, stream, __VA_ARGS__); break;       \
     }                                                                                       \
   } while (0)
 
@@ -75,11 +77,11 @@ extern "C" {
 int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   if (!cfg || !out) return set_error(MHPPO_EINVAL, "null argument");
   *out = nullptr;
-  if (cfg->variant < 0 || cfg->variant > 3) return set_error(MHPPO_EINVAL, "unknown variant %d", cfg->variant);
+  if (cfg->variant < 0 || cfg->variant > 5) return set_error(MHPPO_EINVAL, "unknown variant %d", cfg->variant);
   if (cfg->n_envs <= 0) return set_error(MHPPO_EINVAL, "n_envs must be > 0");
   if (cfg->nb_car < 1 || cfg->nb_ped < 1 || cfg->nb_lines < 1 || cfg->nb_ped > 8)
     return set_error(MHPPO_EINVAL, "bad nb_car/nb_ped/nb_lines");
-  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : cfg->nb_car;
+  int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : (cfg->variant == V_4CARS2 ? 2 : 1) * cfg->nb_car;
   if (nS > MAXS) return set_error(MHPPO_EINVAL, "too many car slots (%d > %d)", nS, MAXS);
   if (cfg->variant == V_SCALABLE && cfg->nb_car > nS)
     return set_error(MHPPO_EINVAL, "scalable: nb_car must be <= 2*nb_lines (random.sample)");
@@ -126,6 +128,7 @@ void mhppo_env_destroy(mhppo_env *env) {
 
 int mhppo_env_obs_dim(const mhppo_env *env) { return env ? env->c.obs_dim : MHPPO_EINVAL; }
 int mhppo_env_slots(const mhppo_env *env) { return env ? env->c.nS : MHPPO_EINVAL; }
+int mhppo_env_reward_slots(const mhppo_env *env) { return env ? env->c.nAV : MHPPO_EINVAL; }
 int mhppo_env_state_dim(const mhppo_env *env) { return env ? 21 * env->c.P + 8 * env->c.nC + 4 : MHPPO_EINVAL; }
 
 int64_t mhppo_env_state_bytes(const mhppo_env *env) { return env ? (int64_t)env->blob_bytes : MHPPO_EINVAL; }

@@ -87,7 +87,11 @@ __device__ __forceinline__ void wave_sync() {
 }
 // scheduling fence between phases: keeps the scheduler from hoisting the next phase's LDS
 // operand reads (and their registers) into the current one
+#ifndef MHPPO_NO_PHASE
 __device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
+#else
+__device__ __forceinline__ void phase() {}
+#endif
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll

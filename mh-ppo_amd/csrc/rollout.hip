@@ -432,7 +432,11 @@ double *scratch(size_t n) {
       case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
       case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;     \
       case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break; \
-      default: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;           \
+      case V_NAIF: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
+      case V_STOP: hipLaunchKernelGGL(kern<V_STOP>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
+      default:                                                                                               \
+        return set_error(MHPPO_EINVAL, "the rollout/evaluation drivers do not support variant %d (4cars2: "    \
+                         "the reference has no driver and its followers earn no reward)", variant);          \
     }                                                                                                        \
   } while (0)
 

@@ -7,7 +7,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmhppo.so")
+# MHPPO_LIB points at an alternative build of the same library (A/B kernel experiments,
+# tools/ab_build.sh); the default is the in-tree build.
+LIB_PATH = os.environ.get("MHPPO_LIB") or os.path.join(HERE, "lib", "libmhppo.so")
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -47,6 +49,7 @@ _SIGS = {
     "mhppo_env_destroy": (None, [P]),
     "mhppo_env_obs_dim": (I32, [P]),
     "mhppo_env_slots": (I32, [P]),
+    "mhppo_env_reward_slots": (I32, [P]),
     "mhppo_env_state_dim": (I32, [P]),
     "mhppo_env_reset": (I32, [P, P, P]),
     "mhppo_env_state_bytes": (I64, [P]),

@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 
-VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3}
+VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3, "4cars2": 4, "stop": 5}
 CAR_B = ((-4.0, 10.0), (2.0, 10.0))   # Coop-MH-PPO-scalable.py:1007
 PED_B = ((-0.05, 0.75, 0.0, -3.0), (0.05, 1.75, 4.0, -0.5))  # :1008
 CROSS_B = (2.5, 3.0)  # :1009
@@ -65,7 +65,8 @@ class VecCrosswalk:
             _lib.check(L.mhppo_env_create(ctypes.byref(cfg), dev_index, ctypes.byref(h)))
         self._h = h
         self.obs_dim = L.mhppo_env_obs_dim(h)
-        self.n_slots = L.mhppo_env_slots(h)
+        self.n_slots = L.mhppo_env_slots(h)              # action slots: actions are [N, 2 * n_slots]
+        self.n_reward_slots = L.mhppo_env_reward_slots(h)  # reward / reward_light width
         self.state_dim = L.mhppo_env_state_dim(h)
 
     @property
@@ -97,8 +98,8 @@ class VecCrosswalk:
         if a.shape != (self.n_envs, 2 * self.n_slots):
             raise ValueError(f"actions must be [{self.n_envs}, {2 * self.n_slots}], got {tuple(a.shape)}")
         obs = self._t((self.n_envs, self.obs_dim), torch.float32) if want_obs else None
-        rew = self._t((self.n_envs, self.n_slots), torch.float64)
-        rl = self._t((self.n_envs, self.n_slots), torch.float64)
+        rew = self._t((self.n_envs, self.n_reward_slots), torch.float64)
+        rl = self._t((self.n_envs, self.n_reward_slots), torch.float64)
         done = self._t((self.n_envs,), torch.uint8)
         _lib.check(_lib.lib().mhppo_env_step(self._h, _lib.ptr(a), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(rl),
                                              _lib.ptr(done), _lib.stream_ptr()))

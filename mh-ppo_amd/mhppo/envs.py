@@ -24,6 +24,8 @@ VARIANT_OF_ID = {
     "Crosswalk_hybrid_multi_coop_4cars-v0": "4cars",
     "Crosswalk_hybrid_multi_coop_scalable-v0": "scalable",
     "Crosswalk_hybrid_multi_naif-v0": "naif",
+    "Crosswalk_hybrid_multi_coop_4cars2-v0": "4cars2",
+    "Crosswalk_hybrid_multi_stop-v0": "stop",
 }
 _REGISTRY = {}
 
@@ -70,15 +72,16 @@ class CrosswalkEnv:
         self.dt, self.max_episode, self.simulation = dt, max_episode, simulation
         self.speed_limit = 10
         self.Vm, self.tau, self.car_size = 2.5, 1.0, 4.0
-        self.S = 2 * nb_lines if variant == "scalable" else nb_car
-        self.nC = 2 * self.S if variant == "4cars" else self.S
+        self.S = 2 * nb_lines if variant == "scalable" else nb_car  # AV slots (rewards, cars[])
+        self.nA = 2 * nb_car if variant == "4cars2" else self.S     # action slots (4cars2: + followers)
+        self.nC = 2 * nb_car if variant in ("4cars", "4cars2") else self.S
         cw = 7 if variant == "scalable" else 6
         spaces = {"car": Box((self.S * cw,)), "env": Box((4 if variant == "scalable" else 3,)),
                   "ped": Box((nb_ped * 9,))}
-        if variant == "4cars":
+        if variant in ("4cars", "4cars2"):
             spaces["car_follow"] = Box((nb_car * 6,))
         self.observation_space = Dict(spaces)
-        self.action_space = Box((2 * self.S,))
+        self.action_space = Box((2 * self.nA,))
         self._seed, self._device, self._backend = seed, device, backend
         self.reward_light = 0.0
         self.state = None
@@ -139,8 +142,8 @@ class CrosswalkEnv:
     def step(self, actions):
         import torch
         a = np.asarray(actions, dtype=np.float64).reshape(1, -1)
-        if a.shape[1] != 2 * self.S:
-            raise ValueError(f"expected {2 * self.S} actions, got {a.shape[1]}")
+        if a.shape[1] != 2 * self.nA:
+            raise ValueError(f"expected {2 * self.nA} actions, got {a.shape[1]}")
         ta = torch.from_numpy(a)
         if hasattr(self.venv, "device"):
             ta = ta.to(self.venv.device)

@@ -32,6 +32,9 @@ class RolloutBatch:
 
 class RolloutGPU:
     def __init__(self, venv, T=None):
+        if venv.variant == "4cars2":
+            raise ValueError("4cars2 is an env-level variant only: the reference has no driver for it and its "
+                             "PPO-driven followers earn no reward (Env_hybrid_multi_coop_4cars2.py:836-847)")
         self.venv = venv
         self.T = T or venv.max_episode
         N, S, P = venv.n_envs, venv.n_slots, venv.nb_ped

@@ -12,7 +12,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
-VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3}
+VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3, "4cars2": 4, "stop": 5}
 CAR_B = np.array([[-4.0, 10.], [2.0, 10.]])
 PED_B = np.array([[-0.05, 0.75, 0.0, -3.0], [0.05, 1.75, 4., -0.5]])
 CROSS_B = np.array([2.5, 3.0])

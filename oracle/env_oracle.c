@@ -35,7 +35,7 @@
 
 #include "pyrandom.h"
 
-enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3 };
+enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP = 5 };
 #define MAXC 16
 #define MAXP 8
 
@@ -150,7 +150,7 @@ static void ped_init(OEnv *e, Ped *p, int is_crossing, int exist) {
     p->ratio = 0.0;
     if (!p->exist) {
         p->init_speed[0] = 0.; p->init_speed[1] = 0.;
-        if (v == V_4CARS || v == V_NAIF) {
+        if (v == V_4CARS || v == V_NAIF || v == V_4CARS2 || v == V_STOP) {
             p->init_pos[0] = e->ped_b[0][2];
             p->init_pos[1] = e->ped_b[0][3] * (double)p->direction;
         } else {
@@ -173,7 +173,7 @@ static void ped_init(OEnv *e, Ped *p, int is_crossing, int exist) {
     if (v == V_COOP) {
         p->need_to_stop = 1;
         p->cross_stop = pyr_uniform(r, -p->cross_lines / 2 + 0.2, p->cross_lines / 2 - 0.2);
-    } else if (v == V_SCALABLE) {
+    } else if (v == V_SCALABLE || v == V_4CARS2 || v == V_STOP) {
         p->need_to_stop = pyr_uniform(r, 0, 1) < 0.5;
         p->cross_stop = pyr_uniform(r, -p->cross_lines / 2 + 0.2, p->cross_lines / 2 - 0.2);
     }
@@ -251,7 +251,7 @@ static int choix_pedestrian(OEnv *e, Ped *p, const CarView *cv) {
                 if (cv->pos[i] < p->Sp_x && cv->light[i] < 0) return 0;
             }
         } else {
-            if (v != V_4CARS && n > 1) {
+            if (v != V_4CARS && v != V_4CARS2 && n > 1) {
                 int tmp[2 * MAXC];
                 for (int i = 0; i < n; i++) tmp[i] = i;
                 pyr_shuffle(&e->rng, tmp, n); /* throw-away list: RNG consumption only */
@@ -315,7 +315,7 @@ static void ped_get_data(const OEnv *e, Ped *p, const CarView *cv, double out[9]
 static double new_reward_wait_safety(const OEnv *e, Ped *p, double car_speed, double car_pos, double car_line) {
     if ((!p->ped_left) * (p->is_crossing) * (car_pos < p->Sp_x) * is_in_front(p, car_line, 0)) {
         double exp_dl;
-        if (car_speed < 0.05) {
+        if (car_speed < (e->variant == V_STOP ? 0.01 : 0.05)) {
             exp_dl = 0.;
         } else {
             double dl = delta_l(e, p, car_pos, car_speed, car_line) / (car_speed);
@@ -410,8 +410,9 @@ static void ped_step(OEnv *e, Ped *p, double time, const CarView *cv) {
                     p->time_before_crossing = p->time_before_crossing + p->dt;
                     p->waiting_time = p->waiting_time + p->dt;
                 }
-            } else if (e->variant == V_SCALABLE && (p->need_to_stop) && p->Sp_y < p->cross_stop && pp_y > p->cross_stop) {
-                p->time_stop = (int)pyr_randint(r, 5, 35);
+            } else if ((e->variant == V_SCALABLE || e->variant == V_4CARS2 || e->variant == V_STOP) &&
+                       (p->need_to_stop) && p->Sp_y < p->cross_stop && pp_y > p->cross_stop) {
+                p->time_stop = (e->variant == V_STOP) ? (int)pyr_randint(r, 2, 15) : (int)pyr_randint(r, 5, 35);
                 p->need_to_stop = 0;
                 if (!p->choose) {
                     p->decision = 0;
@@ -438,7 +439,9 @@ static void ped_step(OEnv *e, Ped *p, double time, const CarView *cv) {
             }
             p->change_line = 0;
         } else {
-            p->time_stop = (int)pyr_randint(r, 2, 5);
+            if (e->variant == V_4CARS2) p->time_stop = (int)pyr_randint(r, 5, 35);
+            else if (e->variant == V_STOP) p->time_stop = (int)pyr_randint(r, 2, 15);
+            else p->time_stop = (int)pyr_randint(r, 2, 5);
             if (!p->choose) {
                 p->decision = 0;
                 p->time_stop = 0;
@@ -480,7 +483,7 @@ static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n,
             else dl = worst_delta_l(e, p, c->Sc, c->Vc, c->line) / (c->Vc);
             double pa;
             if (dl > 0) pa = -1. * exp(-4. * (dl));
-            else pa = (v == V_NAIF) ? -1. * dl - 1 : 1. * dl - 1;
+            else pa = (v == V_NAIF || v == V_STOP) ? -1. * dl - 1 : 1. * dl - 1;
             c->possible_accident = pymin(c->possible_accident, pa);
         }
         if (v == V_NAIF) {
@@ -514,7 +517,7 @@ static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n,
         Car *c = &cars[i];
         double res = c->possible_accident + c->error_scenario;
         double term = 0.5 * green * (double)(c->light < 0.) * (double)(c->Ts > 0);
-        if (v == V_COOP) res = res + term;
+        if (v == V_COOP || v == V_4CARS2 || v == V_STOP) res = res + term;
         else if (v == V_4CARS || v == V_SCALABLE) res = res - term;
         if (v == V_SCALABLE && !c->exist) res = 0.;
         out[i] = res;
@@ -567,6 +570,7 @@ static void car_step(const OEnv *e, Car *c, double action, double light) {
     } else {
         sg = pymax(pymin(-c->Vc / (c->dt * acc), 1.), 0.);
     }
+    if (e->variant == V_STOP && sg > 0.) acc = pymax(acc, -c->Vc / (c->dt * sg)); /* stop :603-605 */
     double final_acc = 0.0;
     final_acc = final_acc + 1.0 * acc;
     final_acc = final_acc + 0. * c->acc_hist[0];
@@ -610,7 +614,8 @@ void oracle_env_get_rng(const OEnv *e, uint32_t *mt, int32_t *mti) {
 
 int oracle_env_obs_dim(const OEnv *e) {
     switch (e->variant) {
-    case V_4CARS: return 12 * e->nb_car + 3 + 9 * e->nb_ped;
+    case V_4CARS:
+    case V_4CARS2: return 12 * e->nb_car + 3 + 9 * e->nb_ped;
     case V_SCALABLE: return 7 * e->nS + 4 + 9 * e->nb_ped;
     default: return 6 * e->nb_car + 3 + 9 * e->nb_ped;
     }
@@ -643,7 +648,7 @@ static void write_obs(OEnv *e, const CarView *pv, float *obs) {
         car_data(e, &e->cars[i], tmp);
         for (int j = 0; j < cw; j++) obs[k++] = (float)tmp[j];
     }
-    if (e->variant == V_4CARS) {
+    if (e->variant == V_4CARS || e->variant == V_4CARS2) {
         for (int i = 0; i < e->nb_car; i++) {
             car_data(e, &e->follow[i], tmp);
             for (int j = 0; j < 6; j++) obs[k++] = (float)tmp[j];
@@ -681,15 +686,15 @@ void oracle_env_reset(OEnv *e, float *obs) {
         }
     } else {
         for (int i = 0; i < e->nb_car; i++) car_init(e, &e->cars[i], (double)(i % e->nb_lines), 0, 1);
-        if (v == V_4CARS)
+        if (v == V_4CARS || v == V_4CARS2)
             for (int i = 0; i < e->nb_car; i++) car_init(e, &e->follow[i], e->cars[i].line, 0, 1);
         e->car_traffic = e->nb_car;
     }
     e->ped_traffic = (int)pyr_randint(r, 1, e->nb_ped);
     for (int i = 0; i < e->ped_traffic; i++) ped_init(e, &e->peds[i], 1, 1);
-    if (v == V_4CARS) {
-        for (int i = 0; i < e->nb_car; i++) { /* reset_car(speed_limit, Sc-15., 0, line) */
-            e->follow[i].Sc = e->cars[i].Sc - 15.;
+    if (v == V_4CARS || v == V_4CARS2) {
+        for (int i = 0; i < e->nb_car; i++) { /* reset_car(speed_limit, Sc-15., 0, line); 4cars2 Sc-U(10,30) */
+            e->follow[i].Sc = e->cars[i].Sc - (v == V_4CARS2 ? pyr_uniform(r, 10, 30) : 15.);
             e->follow[i].Vc = (double)e->speed_limit;
             e->follow[i].light = 0;
             e->follow[i].line = e->cars[i].line;
@@ -720,20 +725,26 @@ int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards,
             }
             a = pymin(idm, a);
         }
-        car_step(e, c, a, actions[i + nS]);
+        /* 4cars2: actions = [AV acc, follower acc, AV light, follower light] (:809-811) */
+        car_step(e, c, a, actions[i + (v == V_4CARS2 ? 2 * nS : nS)]);
     }
-    if (v == V_4CARS) {
+    if (v == V_4CARS || v == V_4CARS2) {
         for (int i = 0; i < e->nb_car; i++) {
             const Car *l = &e->cars[i];
             double a = car_follow_action(e, &e->follow[i], l->Vc, l->Sc);
-            car_step(e, &e->follow[i], a, l->light);
+            double light = l->light;
+            if (v == V_4CARS2) { /* follower step(action_ppo, action_light, leader) (:75-79) */
+                a = pymin(a, actions[nS + i]);
+                light = actions[3 * nS + i];
+            }
+            car_step(e, &e->follow[i], a, light);
         }
     }
     CarView cv;
     cv.n = 0;
     for (int i = 0; i < nS; i++)
         if (v != V_SCALABLE || e->cars[i].exist) view_add(&cv, &e->cars[i]);
-    if (v == V_4CARS)
+    if (v == V_4CARS || v == V_4CARS2)
         for (int i = 0; i < e->nb_car; i++) view_add(&cv, &e->follow[i]);
     for (int p = 0; p < e->nb_ped; p++) ped_step(e, &e->peds[p], e->time, &cv);
 

@@ -27,11 +27,18 @@ CASES = {
     "scalable_432": ("scalable", 4, 3, 2, 8, 450, 80),
     "coop_133": ("coop", 1, 3, 3, 6, 500, 80),
     "naif_221": ("naif", 2, 2, 1, 6, 550, 80),
+    "4cars2_412": ("4cars2", 4, 1, 2, 8, 600, 80),
+    "4cars2_222": ("4cars2", 2, 2, 2, 6, 650, 80),
+    "stop_212": ("stop", 2, 1, 2, 8, 700, 80),
+    "stop_422": ("stop", 4, 2, 2, 8, 750, 80),
 }
 
 
 def n_slots(variant, nb_car, nb_lines):
-    return 2 * nb_lines if variant == "scalable" else nb_car
+    """Action slots: acc + light per slot (4cars2: AVs and PPO-driven followers)."""
+    if variant == "scalable":
+        return 2 * nb_lines
+    return 2 * nb_car if variant == "4cars2" else nb_car
 
 
 def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps):

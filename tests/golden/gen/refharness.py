@@ -31,6 +31,8 @@ IDS = {
     "4cars": "Crosswalk_hybrid_multi_coop_4cars-v0",
     "scalable": "Crosswalk_hybrid_multi_coop_scalable-v0",
     "naif": "Crosswalk_hybrid_multi_naif-v0",
+    "4cars2": "Crosswalk_hybrid_multi_coop_4cars2-v0",
+    "stop": "Crosswalk_hybrid_multi_stop-v0",
 }
 
 

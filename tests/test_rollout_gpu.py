@@ -54,7 +54,8 @@ def test_gpu_rollout_matches_reference(path):
         np.testing.assert_allclose(returns(b["rew_" + h]), g["ret_" + h], rtol=1e-4, atol=1e-4, err_msg=h)
 
 
-@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 1, 4), ("coop", 4, 2, 2)])
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 1, 4), ("coop", 4, 2, 2),
+                                  ("stop", 2, 2, 2)])
 def test_gpu_rollout_matches_oracle_philox(case):
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO

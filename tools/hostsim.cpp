@@ -32,38 +32,29 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
 }
 int hs_obs_dim(HostEnv *h) { return h->c.obs_dim; }
 int hs_state_dim(HostEnv *h) { return 21 * h->c.P + 8 * h->c.nC + 4; }
-void hs_reset(HostEnv *h, float *obs) {
-  for (int e = 0; e < h->c.N; e++) {
-    switch (h->c.variant) {
-      case V_COOP: env_reset_one<V_COOP>(h->c, h->b, e, obs); break;
-      case V_4CARS: env_reset_one<V_4CARS>(h->c, h->b, e, obs); break;
-      case V_SCALABLE: env_reset_one<V_SCALABLE>(h->c, h->b, e, obs); break;
-      default: env_reset_one<V_NAIF>(h->c, h->b, e, obs);
-    }
+#define HS_DISPATCH(call)                                     \
+  switch (h->c.variant) {                                     \
+    case V_COOP: { constexpr int V = V_COOP; call; } break;     \
+    case V_4CARS: { constexpr int V = V_4CARS; call; } break;   \
+    case V_SCALABLE: { constexpr int V = V_SCALABLE; call; } break; \
+    case V_NAIF: { constexpr int V = V_NAIF; call; } break;     \
+    case V_4CARS2: { constexpr int V = V_4CARS2; call; } break; \
+    default: { constexpr int V = V_STOP; call; } break;         \
   }
+int hs_reward_slots(HostEnv *h) { return h->c.nAV; }
+void hs_reset(HostEnv *h, float *obs) {
+  for (int e = 0; e < h->c.N; e++) HS_DISPATCH(env_reset_one<V>(h->c, h->b, e, obs));
 }
 void hs_step(HostEnv *h, const double *a0, float *obs, double *rew0, double *rl0, uint8_t *done) {
-  const int S = h->c.nS;
+  const int S = h->c.nS, R = h->c.nAV;
   for (int e = 0; e < h->c.N; e++) {
     const double *a = a0 + (size_t)e * 2 * S;
-    double *rew = rew0 + (size_t)e * S, *rl = rl0 + (size_t)e * S;
-    switch (h->c.variant) {
-      case V_COOP: env_step_one<V_COOP>(h->c, h->b, e, a, obs, rew, rl, done); break;
-      case V_4CARS: env_step_one<V_4CARS>(h->c, h->b, e, a, obs, rew, rl, done); break;
-      case V_SCALABLE: env_step_one<V_SCALABLE>(h->c, h->b, e, a, obs, rew, rl, done); break;
-      default: env_step_one<V_NAIF>(h->c, h->b, e, a, obs, rew, rl, done);
-    }
+    double *rew = rew0 + (size_t)e * R, *rl = rl0 + (size_t)e * R;
+    HS_DISPATCH(env_step_one<V>(h->c, h->b, e, a, obs, rew, rl, done));
   }
 }
 void hs_state(HostEnv *h, double *out) {
   int dim = hs_state_dim(h);
-  for (int e = 0; e < h->c.N; e++) {
-    switch (h->c.variant) {
-      case V_COOP: env_state_one<V_COOP>(h->c, h->b, e, out, dim); break;
-      case V_4CARS: env_state_one<V_4CARS>(h->c, h->b, e, out, dim); break;
-      case V_SCALABLE: env_state_one<V_SCALABLE>(h->c, h->b, e, out, dim); break;
-      default: env_state_one<V_NAIF>(h->c, h->b, e, out, dim);
-    }
-  }
+  for (int e = 0; e < h->c.N; e++) HS_DISPATCH(env_state_one<V>(h->c, h->b, e, out, dim));
 }
 }
