@@ -33,6 +33,9 @@ extern "C" {
 #define MHPPO_NAIF 3      /* Crosswalk_hybrid_multi_naif-v0          Env_hybrid_multi_naif.py:616 */
 #define MHPPO_4CARS2 4    /* Crosswalk_hybrid_multi_coop_4cars2-v0   Env_hybrid_multi_coop_4cars2.py:683
                              (env only: actions [AV acc, follower acc, AV light, follower light]) */
+/* mhppo_env_cfg.flags */
+#define MHPPO_FIX_SCALABLE_LANES 1 /* scalable: build slot i's car with i (lane i//2, follower 20 m behind
+                                      when i is odd) instead of i//2 (lane (i//2)//2, :900-906, :537, :576) */
 #define MHPPO_STOP 5      /* Crosswalk_hybrid_multi_stop-v0          Env_hybrid_multi_stop.py:634 */
 
 typedef struct mhppo_env_cfg {
@@ -41,7 +44,7 @@ typedef struct mhppo_env_cfg {
     int32_t nb_car, nb_ped, nb_lines;
     int32_t max_episode;  /* 80 in every reference driver */
     int32_t sin_model;    /* simulation == "sin" */
-    int32_t reserved;
+    int32_t flags;        /* opt-in bug fixes, 0 = the reference's behaviour */
     double dt;            /* 0.3 */
     double car_b[4];      /* row-major [[acc_min, v],[acc_max, v]] */
     double ped_b[8];      /* row-major [2][4] */
@@ -208,6 +211,8 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
  * kind 2 = choice actor (n_in <= 32, n_out 2, pairwise softmax): reads value, logp_old,
  *          stats and the GLOBAL action counts counts[0..1] (float64);
  *          grad = d(O(M) Categorical surrogate / M_global^2)/dW, sums[0] += its sum.
+ *          counts == NULL selects the opt-in per-row loss: act[M] (0/1 as
+ *          float) is read and each row contributes its own action's surrogate / M_global.
  * grad: packed torch layout W1 b1 W2 b2 W3 b3 W4 b4 (32 n_in + 4224 + 33 n_out floats).
  * m_global = the global row count (data parallel: all ranks' rows).
  * Per-device workspace: calls on one device must be ordered on one stream. */

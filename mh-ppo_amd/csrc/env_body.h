@@ -152,7 +152,11 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   }
   int car_traffic = c.nb_car;
   if (V == V_SCALABLE) {
-    for (int i = 0; i < c.nS; i++) car_init(E, i, (double)((i / 2) / 2), (double)((i / 2) % 2), 0);
+    // car(..., i//2) then line = (i//2)//2, offset (i//2)%2 (:900-906, :537, :576); the
+    // MHPPO_FIX_SCALABLE_LANES bug-fix passes the slot itself
+    const bool fix = (c.flags & MHPPO_FIX_SCALABLE_LANES) != 0;
+    auto ci = [&](int i) { return fix ? i : i / 2; };
+    for (int i = 0; i < c.nS; i++) car_init(E, i, (double)(ci(i) / 2), (double)(ci(i) % 2), 0);
     car_traffic = E.rng.randint(1, c.nb_car);
     // random.sample(range(S), k) (pool algorithm) draws every index first; the
     // chosen cars are then re-built in sample order (:903-906)
@@ -167,7 +171,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
     }
     for (int k = 0; k < car_traffic; k++) {
       int pick = (int)((order >> (4 * k)) & 15u);
-      car_init(E, pick, (double)((pick / 2) / 2), (double)((pick / 2) % 2), 1);
+      car_init(E, pick, (double)(ci(pick) / 2), (double)(ci(pick) % 2), 1);
     }
   } else {
     for (int i = 0; i < c.nb_car; i++) car_init(E, i, (double)(i % c.nb_lines), 0, 1);
@@ -335,5 +339,6 @@ inline void build_cfg(const mhppo_env_cfg &cfg_, Cfg &c) {
   c.car_high = (c.pb[1][3] * 10.0) / c.pb[1][1];        // high_car_range (:558)
   c.seed_base = cfg->seed_base;
   c.env_off = cfg->env_id_offset;
+  c.flags = cfg->flags;
 }
 }  // namespace mhppo

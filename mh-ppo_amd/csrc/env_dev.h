@@ -59,6 +59,7 @@ struct Cfg {
   // car.__init__ position bounds (:549-560): low/high_car_range, mean_speed_ped (host-computed)
   double car_low, car_high, mean_speed_ped;
   uint64_t seed_base, env_off;
+  int flags, pad2;  // MHPPO_FIX_* (include/mhppo.h)
 };
 
 struct Bufs {

@@ -221,7 +221,8 @@ __device__ __forceinline__ void load_tile_sync(float *slot, const float *X, int 
   const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
   slot[LY::IN_S0 + l] = bload(rsrc((l < 32 || KIND == K_CRITIC) ? ret + row0 : V + row0, nb), vo);
   if (KIND == K_CONT) slot[LY::IN_S1 + l] = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
-  if (KIND == K_CHOICE) slot[LY::IN_S1 + l] = bload(rsrc(lp + row0, nb), vo);
+  if (KIND == K_CHOICE)  // [logp_old 32 | action 32] (the action is read only in per-row mode)
+    slot[LY::IN_S1 + l] = bload(rsrc((l < 32 || act == nullptr) ? lp + row0 : act + row0, nb), vo);
 }
 
 template <int KIND, int KS, bool PF>
@@ -382,15 +383,21 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
         const float pn[2] = {p[0] / sp, p[1] / sp};
         const float eps = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
         const double inv_m2 = inv_m * inv_m;
+        // reference: every row meets every action with the global counts (the M x M
+        // broadcast); per-row mode (counts == NULL, opt-in bug fix): the row's own action
+        // with weight M_global, i.e. the standard mean over rows of the PPO surrogate
+        const int a_row = counts ? 0 : (int)slot[LY::IN_S1 + 32 + j];
         double dlp[2], f = 0.0;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
+          const double w = counts ? counts[k] : (k == a_row ? m_global : 0.0);
           const float pc = pn[k] < eps ? eps : (pn[k] > hi ? hi : pn[k]);
           const double r = exp((double)logf(pc) - old);
           double dfdr;
-          f += counts[k] * surr_and_grad(r, (double)A, dfdr);
+          const double fk = surr_and_grad(r, (double)A, dfdr);
+          if (w != 0.0) f += w * fk;
           const double pass = (pn[k] >= eps && pn[k] <= hi) ? 1.0 : 0.0;
-          dlp[k] = inv_m2 * counts[k] * dfdr * r * pass / (double)pc;  // dL/dpn_k
+          dlp[k] = inv_m2 * w * dfdr * r * pass / (double)pc;  // dL/dpn_k
         }
         if (kh == 0) dacc[0] += f;
         const double sd = (double)sp;
@@ -612,8 +619,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= 32)");
   if (kind == K_CONT && (n_in != NIN_CONT || !act || !logp_old || !stats))
     return set_error(MHPPO_EINVAL, "continuous actor pass needs n_in 13 and act/logp_old/stats");
-  if (kind == K_CHOICE && (!logp_old || !stats || !counts))
-    return set_error(MHPPO_EINVAL, "choice actor pass needs logp_old/stats/counts");
+  if (kind == K_CHOICE && (!logp_old || !stats || (!counts && !act)))
+    return set_error(MHPPO_EINVAL, "choice actor pass needs logp_old/stats and counts (or act for per-row mode)");
   if (M > ((int64_t)1 << 40)) return set_error(MHPPO_EINVAL, "M too large");
   const bool pf = n_in == NIN_CONT && kind != K_CHOICE;
   if (pf && ((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");

@@ -21,7 +21,7 @@ F64 = ctypes.c_double
 class EnvCfg(ctypes.Structure):
     _fields_ = [
         ("variant", I32), ("n_envs", I32), ("nb_car", I32), ("nb_ped", I32), ("nb_lines", I32),
-        ("max_episode", I32), ("sin_model", I32), ("reserved", I32), ("dt", F64),
+        ("max_episode", I32), ("sin_model", I32), ("flags", I32), ("dt", F64),
         ("car_b", F64 * 4), ("ped_b", F64 * 8), ("cross_b", F64 * 2), ("seed_base", U64),
         ("env_id_offset", U64),
     ]

@@ -48,6 +48,7 @@ class Env_rollout:
         self.shape_env_d = self.gpu.dc
         self.seed = 0
         self.iteration = 0
+        self.fix_bucket = False  # opt-in bug fix (Algo_PPO.fix_bucket)
         self.env.reset(want_obs=False)  # the reference's __init__ resets the env (:107)
         self.batch = None
         self.cross = self.wait = self.choice = None
@@ -74,7 +75,7 @@ class Env_rollout:
             self.batch = self.gpu.collect(actor_net_cross, actor_net_wait, actor_net_choice, seed=self.seed,
                                           iteration=self.iteration, forced_choice=forced_choice, eps_tape=eps_tape)
         self.iteration += 1
-        self.cross, self.wait, self.choice = bucket_segments(self.batch)
+        self.cross, self.wait, self.choice = bucket_segments(self.batch, fix_bucket=self.fix_bucket)
         return self.batch
 
     # reference-named views of the collected batch
@@ -167,6 +168,11 @@ class Algo_PPO:
         self.critic_d_lr = 1e-3
         self.actor_d_lr = 3e-4
         self.verbose = True
+        # opt-in bug fixes, off for parity: bucket cars by their closest
+        # pedestrian's decision; per-row choice loss (not the M x M broadcast).  The scalable
+        # lane fix is an env option: VecCrosswalk(..., fix_scalable_lanes=True).
+        self.fix_bucket = False
+        self.fix_choice_loss = False
         for k, v in hyperparameters.items():
             setattr(self, k, v)
 
@@ -194,7 +200,8 @@ class Algo_PPO:
             if m_d > 0:
                 losses["choice"] = ppo.train_model_d(self.actor_net_choice, self.critic_net_choice,
                                                      self.optimizer_actor_choice, self.optimizer_critic_choice,
-                                                     d["obs"], d["act"], d["logp"], d["ret"], m_d, counts)
+                                                     d["obs"], d["act"], d["logp"], d["ret"], m_d, counts,
+                                                     per_row=self.fix_choice_loss)
         self.last_losses = {k: (float(a.item()) / (m_d * m_d if k == "choice" else (m_c if k == "cross" else m_w)),
                                 float(b.item()) / (m_d if k == "choice" else (m_c if k == "cross" else m_w)))
                             for k, (a, b) in losses.items()} if self.verbose else losses
@@ -211,6 +218,7 @@ class Algo_PPO:
         """(:854-917): per iteration rollout.reset() -> one episode per env -> 10 + 10 epochs
         -> reward curves -> rollout.reset() (both resets consume env draws, as in the
         reference); at the end the curves go to load_model/parameters/*.npy (:908-916)."""
+        self.rollout.fix_bucket = self.fix_bucket
         for ep in range(nb_loop):
             self.rollout.reset()
             self.rollout.iterations_rand(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,

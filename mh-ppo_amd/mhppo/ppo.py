@@ -211,11 +211,26 @@ def train_model_c_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_
     return la, lc  # this rank's loss sums (logging only; reduce if needed)
 
 
-def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts):
+def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row=False):
     """One full-batch epoch of Algo_PPO.train_model_d (:818-851) on the fused kernel:
     critic pass -> all-reduce of the advantage sums -> choice-actor pass (O(M) form of the
     M x M Categorical surrogate with the global action counts) -> gradient all-reduce ->
-    Adam.  counts = global (n0, n1) float64.  Returns this rank's (actor, critic) loss sums."""
+    Adam.  counts = global (n0, n1) float64.  per_row=True is the opt-in bug fix (SURVEY
+    §8(f)4): the standard per-row PPO surrogate (each row's own action, mean over rows)
+    instead of the reference's M x M broadcast.  Returns this rank's (actor, critic) loss sums."""
+    if per_row:
+        if critic.n_in > 32:
+            raise ValueError("per-row choice loss needs the fused kernel (n_in <= 32)")
+        gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
+        stats = _allreduce_(sc[1:3].clone())
+        ga, sa, _ = k_mlp_train(KIND_CHOICE, actor, obs, ret, V, act.float(), logp_old, stats, None,
+                                m_global=m_global)
+        _set_grads(critic, gc)
+        _set_grads(actor, ga)
+        _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+        opt_actor.step()
+        opt_critic.step()
+        return sa[0:1], sc[0:1]
     if critic.n_in > 32:
         return train_model_d_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global,
                                       counts)

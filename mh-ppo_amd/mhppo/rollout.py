@@ -156,8 +156,10 @@ def returns_scan(rew, gamma=0.99):
     return out.reshape(rew.shape)
 
 
-def bucket_segments(batch):
+def bucket_segments(batch, fix_bucket=False):
     """Split (env, slot) episode segments into the reference's cross/wait/choice batches.
+    fix_bucket=True (opt-in bug fix) buckets car i by ITS closest
+    pedestrian's decision action_d[i*P + closest_i] instead of the flat action_d[i].
 
     Bucket rule (:489-507): only existing cars (scalable driver); cross when
     action_d[i] <= 0 where action_d is the per-(car, ped) array indexed by the CAR
@@ -166,7 +168,11 @@ def bucket_segments(batch):
     """
     N, S, P, T = batch.N, batch.S, batch.P, batch.T
     a_flat = batch.a_d.reshape(N, S * P)
-    action_d_i = 2 * a_flat[:, :S].to(torch.int32) - 1  # action_d[i], i < S
+    if fix_bucket:
+        a_car = batch.a_d.reshape(N, S, P).gather(2, batch.closest.reshape(N, S, 1).long()).reshape(N, S)
+        action_d_i = 2 * a_car.to(torch.int32) - 1
+    else:
+        action_d_i = 2 * a_flat[:, :S].to(torch.int32) - 1  # action_d[i], i < S
     exist = batch.exist.bool()
     cross = exist & (action_d_i <= 0)
     wait = exist & (action_d_i > 0)

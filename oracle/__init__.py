@@ -56,7 +56,7 @@ def _p(a):
 class OracleEnv:
     """One reference env on its own CPython random stream."""
 
-    def __init__(self, variant, nb_car, nb_ped, nb_lines, dt=0.3, max_episode=80, sin=True, seed=None):
+    def __init__(self, variant, nb_car, nb_ped, nb_lines, dt=0.3, max_episode=80, sin=True, seed=None, flags=0):
         L = lib()
         self.variant = variant
         self.nb_car, self.nb_ped, self.nb_lines = nb_car, nb_ped, nb_lines
@@ -69,6 +69,9 @@ class OracleEnv:
         if not self.h:
             raise ValueError("oracle_env_create rejected the shape")
         self.obs_dim = L.oracle_env_obs_dim(self.h)
+        if flags:
+            L.oracle_env_set_flags.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            L.oracle_env_set_flags(self.h, int(flags))
         if seed is not None:
             L.oracle_env_seed(self.h, seed)
 

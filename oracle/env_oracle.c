@@ -101,6 +101,7 @@ typedef struct {
 typedef struct {
     int variant, nb_car, nb_ped, nb_lines, max_episode, sin_model;
     double dt, car_b[2][2], ped_b[2][4], cross_b[2];
+    int flags;
     PyRandom rng;
     double cross;
     int speed_limit;
@@ -605,6 +606,8 @@ OEnv *oracle_env_create(int variant, int nb_car, int nb_ped, int nb_lines, doubl
 }
 
 void oracle_env_destroy(OEnv *e) { free(e); }
+/* opt-in bug fixes (include/mhppo.h MHPPO_FIX_*), never set for parity runs */
+void oracle_env_set_flags(OEnv *e, int flags) { e->flags = flags; }
 void oracle_env_seed(OEnv *e, uint64_t seed) { pyr_seed(&e->rng, seed); }
 uint64_t oracle_env_rng_words(const OEnv *e) { return e->rng.words; }
 void oracle_env_get_rng(const OEnv *e, uint32_t *mt, int32_t *mti) {
@@ -676,13 +679,17 @@ void oracle_env_reset(OEnv *e, float *obs) {
     e->speed_limit = 10;
     for (int i = 0; i < e->nb_ped; i++) ped_init(e, &e->peds[i], 0, 0);
     if (v == V_SCALABLE) {
-        for (int i = 0; i < e->nS; i++) car_init(e, &e->cars[i], (double)((i / 2) / 2), (double)((i / 2) % 2), 0);
+        const int fix = e->flags & 1; /* MHPPO_FIX_SCALABLE_LANES: car(..., i) instead of car(..., i//2) */
+        for (int i = 0; i < e->nS; i++) {
+            int ci = fix ? i : i / 2;
+            car_init(e, &e->cars[i], (double)(ci / 2), (double)(ci % 2), 0);
+        }
         e->car_traffic = (int)pyr_randint(r, 1, e->nb_car);
         int nums[MAXC];
         pyr_sample_range(r, e->nS, e->car_traffic, nums);
         for (int k = 0; k < e->car_traffic; k++) {
-            int i = nums[k];
-            car_init(e, &e->cars[i], (double)((i / 2) / 2), (double)((i / 2) % 2), 1);
+            int i = nums[k], ci = fix ? i : i / 2;
+            car_init(e, &e->cars[i], (double)(ci / 2), (double)(ci % 2), 1);
         }
     } else {
         for (int i = 0; i < e->nb_car; i++) car_init(e, &e->cars[i], (double)(i % e->nb_lines), 0, 1);
