@@ -33,10 +33,12 @@ extern "C" {
 #define MHPPO_NAIF 3      /* Crosswalk_hybrid_multi_naif-v0          Env_hybrid_multi_naif.py:616 */
 #define MHPPO_4CARS2 4    /* Crosswalk_hybrid_multi_coop_4cars2-v0   Env_hybrid_multi_coop_4cars2.py:683
                              (env only: actions [AV acc, follower acc, AV light, follower light]) */
+#define MHPPO_STOP 5      /* Crosswalk_hybrid_multi_stop-v0          Env_hybrid_multi_stop.py:634 */
 /* mhppo_env_cfg.flags */
 #define MHPPO_FIX_SCALABLE_LANES 1 /* scalable: build slot i's car with i (lane i//2, follower 20 m behind
                                       when i is odd) instead of i//2 (lane (i//2)//2, :900-906, :537, :576) */
-#define MHPPO_STOP 5      /* Crosswalk_hybrid_multi_stop-v0          Env_hybrid_multi_stop.py:634 */
+#define MHPPO_GENERIC_STEP 2       /* not a semantic flag: always run the step on the generic in-HBM env view
+                                      (the register view serves the shapes it is compiled for; tests compare both) */
 
 typedef struct mhppo_env_cfg {
     int32_t variant;      /* MHPPO_* */

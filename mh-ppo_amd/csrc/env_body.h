@@ -10,10 +10,23 @@
 namespace mhppo {
 constexpr int MAXS = 16;  // AV slots per env (scalable 2*nb_lines, coop nb_car)
 
+// Shapes (variant, nC, nAV, P) with a register-view step kernel: the benchmark configs
+// (coop 2/1/2, 4cars 4/1/2, scalable 8/1/4) and the other single-pedestrian fixture
+// shapes (stop 2/1/2, 4cars2 4/1/2).  Every other shape runs on the generic view.
+// (Multi-pedestrian shapes are left generic: fully unrolling ped_step per pedestrian
+// exceeds the unroller's budget and a runtime-indexed array would live in scratch.)
+#define MHPPO_REG_SHAPES(X) \
+  X(V_COOP, 2, 2, 1) X(V_4CARS, 8, 4, 1) X(V_SCALABLE, 8, 8, 1) X(V_STOP, 2, 2, 1) X(V_4CARS2, 8, 4, 1)
+
+inline bool use_reg_view(const Cfg &c, int V_, int NC, int NAV, int NP) {
+  return !(c.flags & MHPPO_GENERIC_STEP) && c.variant == V_ && c.nC == NC && c.nAV == NAV && c.P == NP;
+}
+
 // ----------------------------------------------------------------- reset
-template <int V>
-MHPPO_HD void ped_init(Env<V> &E, Ped &q, int is_crossing, int exist) {
-  Rng &r = E.rng;
+template <class EV>
+MHPPO_HD void ped_init(EV &E, Ped &q, int is_crossing, int exist) {
+  constexpr int V = EV::VAR;
+  auto &r = E.rng;
   const Cfg &c = E.c;
   q = Ped{};
   q.wdl = 0.0;
@@ -72,8 +85,9 @@ MHPPO_HD void ped_init(Env<V> &E, Ped &q, int is_crossing, int exist) {
   }
 }
 
-template <int V>
-MHPPO_HD void car_init(Env<V> &E, int s, double line, double offset, int exist) {
+template <class EV>
+MHPPO_HD void car_init(EV &E, int s, double line, double offset, int exist) {
+  constexpr int V = EV::VAR;
   const Cfg &c = E.c;
   double finish = (E.cl * 10.0) / (c.mean_speed_ped);
   double Sc = E.rng.uniform(c.car_low - finish, c.car_high);
@@ -92,8 +106,9 @@ MHPPO_HD void car_init(Env<V> &E, int s, double line, double offset, int exist) 
 }
 
 // car.get_data for the flat obs (coop :609-612, scalable :652-655)
-template <int V>
-MHPPO_HD int write_car_obs(const Env<V> &E, int s, float *o) {
+template <class EV>
+MHPPO_HD int write_car_obs(const EV &E, int s, float *o) {
+  constexpr int V = EV::VAR;
   if (V == V_SCALABLE) {
     if (E.car(C_EXIST, s) == 0.0) {
       o[0] = 0.f; o[1] = 0.f; o[2] = 10.f; o[3] = -1000.f; o[4] = 0.f; o[5] = (float)E.car(C_LINE, s); o[6] = 0.f;
@@ -112,23 +127,26 @@ MHPPO_HD int write_car_obs(const Env<V> &E, int s, float *o) {
 
 // flat obs (gym-sorted car|car_follow|env|ped); ped.get_data runs even without
 // an obs buffer because it advances the running-min `delta` (:441).
-template <int V>
-MHPPO_HD void env_observe(Env<V> &E, int mode, float *obs) {
+template <class EV>
+MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
+  constexpr int V = EV::VAR;
   const Cfg &c = E.c;
   float *o = obs ? obs + (size_t)E.e * c.obs_dim : nullptr;
   float tmp[8];
   int k = 0;
   if (o) {
-    for (int s = 0; s < c.nC; s++) {
+    MHPPO_UNROLL
+    for (int s = 0; s < E.nC(); s++) {
       int w = write_car_obs(E, s, tmp);
       for (int j = 0; j < w; j++) o[k++] = tmp[j];
     }
     o[k++] = (float)(E.cross * (double)c.nb_lines / 2.);
-    o[k++] = (float)E.b.envi[EI_PEDTRAF * c.N + E.e];
-    if (V == V_SCALABLE) o[k++] = (float)E.b.envi[EI_CARTRAF * c.N + E.e];
+    o[k++] = (float)E.ped_traffic();
+    if (V == V_SCALABLE) o[k++] = (float)E.car_traffic();
     o[k++] = (float)c.nb_lines;
   }
-  for (int p = 0; p < c.P; p++) {
+  MHPPO_UNROLL
+  for (int p = 0; p < E.nP(); p++) {
     Ped q = load_ped(E, p);
     double d[9];
     ped_get_data(E, q, mode, d);
@@ -202,14 +220,19 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
 
 // ------------------------------------------------------------------ step
 // act: this env's [2 nS] actions [acc..., light...]; rw/rl: this env's [nAV] outputs (nullable)
-template <int V>
-MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act, float *obs, double *rw,
-                           double *rl, uint8_t *done) {
-  Env<V> E(c, b, e);
-  const int nS = c.nAV;  // AV slots (4cars2: followers handled below)
+// act: [2 nS] (pointer or array type); per-AV rewards land in E.rw / E.rl
+template <class EV, class ACT>
+MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
+  constexpr int V = EV::VAR;
+  const Cfg &c = E.c;
+  const Bufs &b = E.b;
+  const int e = E.e;
+  const int nS = E.nAV();  // AV slots (4cars2: followers handled below)
   double time = b.envd[E_TIME * c.N + e];
-  double prev[MAXS];
+  typename EV::AvArr prev, acc;
+  MHPPO_UNROLL
   for (int i = 0; i < nS; i++) prev[i] = E.car(C_SC, i);
+  MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
     double a = act[i];
     if (V == V_SCALABLE) {
@@ -218,39 +241,45 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
         idm = car_follow_action(E, i, E.car(C_VC, i - 1), E.car(C_SC, i - 1));
       a = pymin(idm, a);
     }
-    car_step(E, i, a, act[i + c.nS]);
+    car_step(E, i, a, act[i + E.nS()]);
   }
-  if (has_followers(V))
-    for (int i = 0; i < c.nb_car; i++) {
+  if (has_followers(V)) {
+    MHPPO_UNROLL
+    for (int i = 0; i < nS; i++) {  // one follower per AV (nb_car == nAV)
       double a = car_follow_action(E, nS + i, E.car(C_VC, i), E.car(C_SC, i));
       double light = E.car(C_LIGHT, i);
       if (V == V_4CARS2) {  // follower step(action_ppo, action_light, leader) (:75-79, :811)
         a = pymin(a, act[nS + i]);
-        light = act[c.nS + nS + i];
+        light = act[E.nS() + nS + i];
       }
       car_step(E, nS + i, a, light);
     }
-  for (int p = 0; p < c.P; p++) {
+  }
+  MHPPO_UNROLL
+  for (int p = 0; p < E.nP(); p++) {
     Ped q = load_ped(E, p);
     ped_step(E, q, time);
     store_ped(E, p, q, true);
   }
-  double acc[MAXS];
+  MHPPO_UNROLL
   for (int i = 0; i < nS; i++) acc[i] = 0.;
-  for (int p = 0; p < c.P; p++) {
+  MHPPO_UNROLL
+  for (int p = 0; p < E.nP(); p++) {
     Ped q = load_ped(E, p);
     bool add = q.has(F_ISCROSS) && (V != V_SCALABLE || q.has(F_EXIST));
-    ped_detection<V, MAXS>(E, q, prev, acc, add);
+    ped_detection(E, q, prev, acc, add);
     E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
   }
+  MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
-    if (rl) rl[i] = acc[i];
+    E.rl[i] = acc[i];
     double Vc = E.car(C_VC, i);
     double r = car_reward(Vc);
     if (E.car(C_LIGHT, i) > 0.0) {
       bool have = false;
       double mn = 0.;
-      for (int p = 0; p < c.P; p++) {
+      MHPPO_UNROLL
+      for (int p = 0; p < E.nP(); p++) {
         uint32_t fl = E.pflag(p);
         if (!(fl & F_EXIST)) continue;
         Ped q = load_ped(E, p);
@@ -261,19 +290,34 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
       }
       if (have) r += mn;
     }
-    if (rw) rw[i] = r;
+    E.rw[i] = r;
   }
   env_observe(E, 1, obs);
-  int d = (time >= c.ep_len) || (b.envi[EI_PEDTRAF * c.N + e] <= 0);
+  int d = (time >= c.ep_len) || (E.ped_traffic() <= 0);
   if (done) done[e] = (uint8_t)d;
   b.envd[E_TIME * c.N + e] = time + c.dt;
-  E.save_rng();
+  E.commit();
 }
+
+template <int V>
+MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act, float *obs, double *rw,
+                           double *rl, uint8_t *done) {
+  Env<V> E(c, b, e);
+  env_step_body(E, act, obs, done);
+  for (int i = 0; i < c.nAV; i++) {
+    if (rw) rw[i] = E.rw[i];
+    if (rl) rl[i] = E.rl[i];
+  }
+}
+
 
 // ------------------------------------------------------------- seeding
 MHPPO_HD inline void env_seed_one(const Cfg &c, const Bufs &b, int e) {
-  rng_seed(b.mt + (size_t)e * 624, c.seed_base + c.env_off + (uint64_t)e);
-  b.envi[EI_MTI * c.N + e] = 624;
+  uint32_t *blk = b.mt + (size_t)e * (MT_BLOCKS * MT_N);
+  rng_seed(blk, c.seed_base + c.env_off + (uint64_t)e);
+  mt_twist_into(blk, blk + MT_N);  // next block ready: active 0, not stale
+  b.envi[EI_MTI * c.N + e] = MT_N;
+  b.envi[EI_MTB * c.N + e] = 0;
   b.envd[E_CROSS * c.N + e] = 0.0;
   b.envd[E_TIME * c.N + e] = 0.0;
 }

@@ -3,7 +3,7 @@
 // State lives in HBM as structure-of-arrays, field-major with the env index
 // fastest ([field][slot][N]), so every per-lane access of a wave is one
 // coalesced 512-B transaction.  Each env draws from its own CPython-compatible
-// MT19937 stream (state [N][624] u32 + cursor), so trajectories are the
+// MT19937 stream (two blocks [N][2][624] u32 + cursor), so trajectories are the
 // reference's on `random.seed(seed_base + env_id)` and invariant to how envs
 // are sharded over GPUs.
 //
@@ -25,7 +25,11 @@
 
 // Every env routine is __host__ __device__: the kernels run it on gfx950 and
 // tools/hostsim.cpp runs the identical source on the CPU for debugging.
-#define MHPPO_HD __host__ __device__
+// Always inlined: an env view passed by reference to an outlined call would have to
+// live in memory (scratch), defeating the register view below.
+#define MHPPO_HD __host__ __device__ __attribute__((always_inline))
+// full unroll of slot/pedestrian loops: compile-time trip counts in the register view
+#define MHPPO_UNROLL _Pragma("unroll")
 
 namespace mhppo {
 
@@ -49,7 +53,7 @@ enum : uint32_t {
 };
 // env scalars
 enum { E_CROSS, E_TIME, E_ND };
-enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_NI };
+enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_MTB, EI_NI };
 
 struct Cfg {
   // nS: action slots (acc + light each); nAV: AV slots with rewards/detection (= nS except
@@ -68,7 +72,7 @@ struct Bufs {
   uint32_t *pfl;  // [P][N]
   double *envd;   // [E_ND][N]
   int32_t *envi;  // [EI_NI][N]
-  uint32_t *mt;   // [N][624]
+  uint32_t *mt;   // [N][2][624] (active + next block, see RngT)
 };
 
 MHPPO_HD __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
@@ -78,27 +82,71 @@ static constexpr double PI = 0x1.921fb54442d18p+1;
 static constexpr double NV_MAGICCONST = 0x1.b72cd3f331398p+0;  // 4*exp(-0.5)/sqrt(2.0)
 
 // ------------------------------------------------------------ CPython random
-struct Rng {
-  uint32_t *mt;  // this env's 624 words
-  int mti;
+// Each env owns TWO 624-word MT19937 blocks, [N][2][624]: the active block (the
+// CPython state, consumed at cursor mti) and the next block = twist(active), kept
+// ready ahead of time.  Exhausting the active block just switches blocks; the old
+// block is marked stale and regenerated as twist(new active) by the whole wave at
+// the start of the next env kernel (mt_refill_wave: coalesced loads, three LDS
+// phases, coalesced stores), so the 624-step twist never sits on one lane's
+// critical path.  envi[EI_MTB]: bit 0 = active block, bit 1 = the other block is stale.
+enum : int { MT_N = 624, MT_BLOCKS = 2 };
 
+MHPPO_HD inline uint32_t mt_mix(uint32_t a, uint32_t b) {  // one twist term of (a, successor b)
+  uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// dst = twist(src), out of place (CPython genrand_uint32's in-place loop restated:
+// terms 0..226 read src only, 227..622 the new words 227 behind, 623 new[396] and new[0])
+__host__ __device__ __attribute__((noinline)) inline void mt_twist_into(const uint32_t *src, uint32_t *dst) {
+  for (int kk = 0; kk < 227; kk++) dst[kk] = src[kk + 397] ^ mt_mix(src[kk], src[kk + 1]);
+  for (int kk = 227; kk < 623; kk++) dst[kk] = dst[kk - 227] ^ mt_mix(src[kk], src[kk + 1]);
+  dst[623] = dst[396] ^ mt_mix(src[623], dst[0]);
+}
+
+// K > 0: the next K words of the active block are read ahead in one batch (independent
+// loads) and consumed in order; an empty window is refilled with one batch, so a run
+// of draws costs one HBM round trip per K words.
+template <int K>
+struct RngT {
+  uint32_t *base;  // this env's two blocks
+  uint32_t *mt;    // the active block
+  int mti, mtb;
+  uint32_t win[K > 0 ? K : 1];  // win[0 .. nwin) == mt[mti .. mti + nwin)
+  int nwin = 0;
+
+  MHPPO_HD void attach(uint32_t *env_blocks, int mti_, int mtb_) {
+    base = env_blocks;
+    mti = mti_;
+    mtb = mtb_;
+    mt = base + (mtb & 1) * MT_N;
+  }
+  MHPPO_HD void prefetch() {
+    if (K == 0) return;
+    nwin = (MT_N - mti) < K ? (MT_N - mti) : K;
+#pragma unroll
+    for (int k = 0; k < (K > 0 ? K : 1); k++) win[k] = (k < nwin) ? mt[mti + k] : 0u;
+  }
   MHPPO_HD uint32_t genrand() {
-    if (mti >= 624) {
-      uint32_t y;
-      int kk;
-      for (kk = 0; kk < 624 - 397; kk++) {
-        y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-        mt[kk] = mt[kk + 397] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-      for (; kk < 623; kk++) {
-        y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-        mt[kk] = mt[kk - 227] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-      y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
-      mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    if (mti >= MT_N) {
+      uint32_t *next = base + ((mtb & 1) ^ 1) * MT_N;
+      if (mtb & 2) mt_twist_into(mt, next);  // next block not regenerated yet (>624 draws in one launch)
+      mtb = ((mtb & 1) ^ 1) | 2;             // switch; the old block is now stale
+      mt = next;
       mti = 0;
+      nwin = 0;
     }
-    uint32_t y = mt[mti++];
+    uint32_t y;
+    if (K > 0) {
+      if (nwin == 0) prefetch();
+      y = win[0];
+#pragma unroll
+      for (int k = 0; k + 1 < (K > 0 ? K : 1); k++) win[k] = win[k + 1];
+      nwin--;
+    } else {
+      y = mt[mti];
+    }
+    mti++;
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
@@ -131,6 +179,7 @@ struct Rng {
     return mu + z * sigma;
   }
 };
+using Rng = RngT<0>;
 
 // init_by_array([seed lo, seed hi]) exactly as CPython's random.seed(int)
 MHPPO_HD inline void rng_seed(uint32_t *mt, uint64_t seed) {
@@ -170,12 +219,29 @@ MHPPO_HD inline double py_floordiv(double vx, double wx) {
   return fl;
 }
 
-// ---------------------------------------------------------------- env view
-// One lane's view of its env.  Car/ped fields are read and written in place
-// in HBM (coalesced across the wave); the pedestrian being stepped is staged
-// in registers (struct Ped) for the duration of its update.
+// ---------------------------------------------------------- small arrays
+template <class T, int N>
+struct PlainArr {
+  T v[N];
+  MHPPO_HD T &operator[](int i) { return v[i]; }
+  MHPPO_HD const T &operator[](int i) const { return v[i]; }
+};
+
+// ---------------------------------------------------------------- env views
+// Every env routine below is written against an "env view" EV: VAR (the variant),
+// shape queries nC()/nAV()/nS()/nP(), MAXAV (capacity of per-AV scratch arrays),
+// accessors car(f, s) / pedf(f, p) / pflag(p), the RNG stream, cross/cl, and
+// commit() (end of a step).  Two views exist:
+//
+// Env<V>: generic shapes.  Car/ped fields are read and written in place in HBM
+// (coalesced across the wave); used by reset, state dumps and every shape the
+// register view is not instantiated for.
 template <int V>
 struct Env {
+  static constexpr int VAR = V;
+  static constexpr int MAXAV = 16;
+  using AvArr = PlainArr<double, MAXAV>;
+  AvArr rw, rl;  // step outputs per AV: reward, reward_light
   const Cfg &c;
   const Bufs &b;
   int e;
@@ -183,16 +249,103 @@ struct Env {
   double cross, cl;  // crosswalk lane width, cross_lines = nb_lines * cross
 
   MHPPO_HD Env(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
-    rng.mt = b.mt + (size_t)e * 624;
-    rng.mti = b.envi[EI_MTI * c.N + e];
+    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[EI_MTI * c.N + e], b.envi[EI_MTB * c.N + e]);
     cross = b.envd[E_CROSS * c.N + e];
     cl = (double)c.nb_lines * cross;
   }
-  MHPPO_HD void save_rng() { b.envi[EI_MTI * c.N + e] = rng.mti; }
+  MHPPO_HD void save_rng() {
+    b.envi[EI_MTI * c.N + e] = rng.mti;
+    b.envi[EI_MTB * c.N + e] = rng.mtb;
+  }
+  MHPPO_HD void commit() { save_rng(); }
+  MHPPO_HD int nC() const { return c.nC; }
+  MHPPO_HD int nAV() const { return c.nAV; }
+  MHPPO_HD int nS() const { return c.nS; }
+  MHPPO_HD int nP() const { return c.P; }
+  MHPPO_HD int ped_traffic() const { return b.envi[EI_PEDTRAF * c.N + e]; }
+  MHPPO_HD int car_traffic() const { return b.envi[EI_CARTRAF * c.N + e]; }
 
   MHPPO_HD double &car(int f, int s) const { return b.car[((size_t)f * c.nC + s) * c.N + e]; }
   MHPPO_HD double &pedf(int f, int p) const { return b.ped[((size_t)f * c.P + p) * c.N + e]; }
   MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[(size_t)p * c.N + e]; }
+};
+
+// EnvR<V, NC, NAV, NP>: compile-time shape (NC car slots, NAV AVs, NP pedestrians).
+// The whole env state is loaded into registers in one batch of independent loads at
+// construction (plus a 16-word RNG window), the step runs on registers with fully
+// unrolled slot/ped loops (every index a compile-time constant after unrolling and
+// inlining, so the arrays below live in VGPRs/AGPRs, never in scratch), and commit()
+// writes the dynamic fields back.  With one env
+// per lane and 65 536 envs the GPU holds one wave per SIMD, so the in-place HBM view
+// serialises ~100 dependent memory round trips per step; this view needs ~3.
+template <int V, int NC, int NAV, int NP>
+struct EnvR {
+  static constexpr int VAR = V;
+  static constexpr int MAXAV = NAV;
+  using AvArr = PlainArr<double, NAV>;
+  AvArr rw, rl;  // step outputs per AV: reward, reward_light
+  const Cfg &c;
+  const Bufs &b;
+  int e;
+  RngT<16> rng;
+  double cross, cl;
+  mutable double car_[C_NF][NC];
+  mutable double ped_[P_NF][NP];
+  mutable uint32_t pfl_[NP];
+  int ptraf, ctraf;
+
+  MHPPO_HD EnvR(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
+    const size_t N = (size_t)c.N;
+    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[EI_MTI * N + e], b.envi[EI_MTB * N + e]);
+    cross = b.envd[E_CROSS * N + e];
+    cl = (double)c.nb_lines * cross;
+    ptraf = b.envi[EI_PEDTRAF * N + e];
+    ctraf = b.envi[EI_CARTRAF * N + e];
+#pragma unroll
+    for (int f = 0; f < C_NF; f++)
+#pragma unroll
+      for (int s = 0; s < NC; s++) car_[f][s] = b.car[((size_t)f * NC + s) * N + e];
+#pragma unroll
+    for (int f = 0; f < P_NF; f++)
+#pragma unroll
+      for (int p = 0; p < NP; p++) ped_[f][p] = b.ped[((size_t)f * NP + p) * N + e];
+#pragma unroll
+    for (int p = 0; p < NP; p++) pfl_[p] = b.pfl[(size_t)p * N + e];
+    rng.prefetch();
+  }
+  // dynamic fields only: line/exist and the pedestrian's static draws never change in a step
+  MHPPO_HD void commit() {
+    const size_t N = (size_t)c.N;
+    constexpr int dyn_car[6] = {C_AC, C_VC, C_SC, C_LIGHT, C_H0, C_H1};
+    constexpr int det_car[3] = {C_PA, C_ES, C_TS};
+    constexpr int dyn_ped[10] = {P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS};
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+      for (int s = 0; s < NC; s++) b.car[((size_t)dyn_car[k] * NC + s) * N + e] = car_[dyn_car[k]][s];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+      for (int s = 0; s < NAV; s++) b.car[((size_t)det_car[k] * NC + s) * N + e] = car_[det_car[k]][s];
+#pragma unroll
+    for (int k = 0; k < 10; k++)
+#pragma unroll
+      for (int p = 0; p < NP; p++) b.ped[((size_t)dyn_ped[k] * NP + p) * N + e] = ped_[dyn_ped[k]][p];
+#pragma unroll
+    for (int p = 0; p < NP; p++) b.pfl[(size_t)p * N + e] = pfl_[p];
+    b.envi[EI_MTI * N + e] = rng.mti;
+    b.envi[EI_MTB * N + e] = rng.mtb;
+  }
+  static constexpr int nC() { return NC; }
+  static constexpr int nAV() { return NAV; }
+  static constexpr int nS() { return V == V_4CARS2 ? 2 * NAV : NAV; }
+  static constexpr int nP() { return NP; }
+  MHPPO_HD int ped_traffic() const { return ptraf; }
+  MHPPO_HD int car_traffic() const { return ctraf; }
+
+  MHPPO_HD double &car(int f, int s) const { return car_[f][s]; }
+  MHPPO_HD double &pedf(int f, int p) const { return ped_[f][p]; }
+  MHPPO_HD uint32_t &pflag(int p) const { return pfl_[p]; }
 };
 
 struct Ped {
@@ -203,8 +356,9 @@ struct Ped {
   MHPPO_HD void set(uint32_t f, bool v) { fl = v ? (fl | f) : (fl & ~f); }
 };
 
-template <int V>
-MHPPO_HD inline Ped load_ped(const Env<V> &E, int p) {
+template <class EV>
+MHPPO_HD inline Ped load_ped(const EV &E, int p) {
+  constexpr int V = EV::VAR;
   Ped q;
   q.Sx = E.pedf(P_SX, p); q.Sy = E.pedf(P_SY, p); q.Vx = E.pedf(P_VX, p); q.Vy = E.pedf(P_VY, p);
   q.t0 = E.pedf(P_T0, p); q.wt = E.pedf(P_WT, p); q.ct = E.pedf(P_CT, p); q.wdl = E.pedf(P_WDL, p);
@@ -217,8 +371,9 @@ MHPPO_HD inline Ped load_ped(const Env<V> &E, int p) {
   return q;
 }
 
-template <int V>
-MHPPO_HD inline void store_ped(const Env<V> &E, int p, Ped &q, bool dyn_only) {
+template <class EV>
+MHPPO_HD inline void store_ped(const EV &E, int p, Ped &q, bool dyn_only) {
+  constexpr int V = EV::VAR;
   E.pedf(P_SX, p) = q.Sx; E.pedf(P_SY, p) = q.Sy; E.pedf(P_VX, p) = q.Vx; E.pedf(P_VY, p) = q.Vy;
   E.pedf(P_T0, p) = q.t0; E.pedf(P_WT, p) = q.wt; E.pedf(P_CT, p) = q.ct; E.pedf(P_WDL, p) = q.wdl;
   E.pedf(P_DELTA, p) = q.delta; E.pedf(P_LPOS, p) = q.lpos;
@@ -234,16 +389,18 @@ MHPPO_HD inline void store_ped(const Env<V> &E, int p, Ped &q, bool dyn_only) {
 }
 
 // ------------------------------------------------------- pedestrian geometry
-template <int V>
-MHPPO_HD inline bool is_in_front(const Env<V> &E, const Ped &q, double car_line, double next_line) {
+template <class EV>
+MHPPO_HD inline bool is_in_front(const EV &E, const Ped &q, double car_line, double next_line) {
+  constexpr int V = EV::VAR;
   double line_1 = (-E.cl / 2) + E.cross * (car_line - 0.5 * next_line + 1);
   double line_2 = (E.cl / 2) - E.cross * ((double)E.c.nb_lines - 0.5 * next_line - car_line);
   if (q.dir == -1) return q.Sy >= line_2 - 0.001;
   return q.Sy <= line_1 + 0.001;
 }
 
-template <int V>
-MHPPO_HD inline bool is_crossing_in_front(const Env<V> &E, const Ped &q, double car_line, double prev_line) {
+template <class EV>
+MHPPO_HD inline bool is_crossing_in_front(const EV &E, const Ped &q, double car_line, double prev_line) {
+  constexpr int V = EV::VAR;
   double line_1 = (-E.cl / 2) + E.cross * (car_line - prev_line);
   double line_2 = (E.cl / 2) - E.cross * ((double)E.c.nb_lines - car_line - 1 - prev_line);
   if (q.dir == -1) return q.Sy < line_2;
@@ -252,15 +409,17 @@ MHPPO_HD inline bool is_crossing_in_front(const Env<V> &E, const Ped &q, double 
 
 // which car slots the pedestrians see: mode 0 = reset observation (all AV slots),
 // mode 1 = step (existing AVs [+ followers for 4cars])
-template <int V>
-MHPPO_HD inline bool in_view(const Env<V> &E, int s, int mode) {
-  if (has_followers(V)) return mode == 1 || s < E.c.nAV;
+template <class EV>
+MHPPO_HD inline bool in_view(const EV &E, int s, int mode) {
+  constexpr int V = EV::VAR;
+  if (has_followers(V)) return mode == 1 || s < E.nAV();
   if (V == V_SCALABLE) return mode == 0 || E.car(C_EXIST, s) != 0.0;
   return true;
 }
 
-template <int V>
-MHPPO_HD inline double CG_score(Env<V> &E, const Ped &q, double crossing_size) {
+template <class EV>
+MHPPO_HD inline double CG_score(EV &E, const Ped &q, double crossing_size) {
+  constexpr int V = EV::VAR;
   if (!q.has(F_ISCROSS)) return 0.;
   const double fem = 0.0369, child = -0.0355, midage = -0.0221, old = -0.1810;
   const double alpha = 0.09, sigma = 0.09;
@@ -272,11 +431,13 @@ MHPPO_HD inline double CG_score(Env<V> &E, const Ped &q, double crossing_size) {
   return pow(10.0, log_val);
 }
 
-template <int V>
-MHPPO_HD inline bool choix_pedestrian(Env<V> &E, const Ped &q, int mode) {
+template <class EV>
+MHPPO_HD inline bool choix_pedestrian(EV &E, const Ped &q, int mode) {
+  constexpr int V = EV::VAR;
   const double car_size = 4;
   int n = 0;
-  for (int s = 0; s < E.c.nC; s++) n += in_view(E, s, mode);
+  MHPPO_UNROLL
+  for (int s = 0; s < E.nC(); s++) n += in_view(E, s, mode);
   if (q.has(F_FOLLOW)) {
     if (V == V_NAIF) {
       // random.shuffle(cars): real permutation, nibble-packed (n <= 16)
@@ -305,21 +466,24 @@ MHPPO_HD inline bool choix_pedestrian(Env<V> &E, const Ped &q, int mode) {
     } else {
       if (!has_followers(V) && n > 1)
         for (int i = n - 1; i >= 1; i--) (void)E.rng.randbelow((uint32_t)(i + 1));
-      for (int s = 0; s < E.c.nC; s++) {
+      MHPPO_UNROLL
+      for (int s = 0; s < E.nC(); s++) {
         if (!in_view(E, s, mode)) continue;
         double pos = E.car(C_SC, s), line = E.car(C_LINE, s);
         if (is_crossing_in_front(E, q, line, 0.5) && is_in_front(E, q, line, 1.0)) {
           if ((pos < car_size + q.Sx) && (pos > q.Sx)) return false;
         }
       }
-      for (int s = 0; s < E.c.nC; s++) {
+      MHPPO_UNROLL
+      for (int s = 0; s < E.nC(); s++) {
         if (!in_view(E, s, mode)) continue;
         double light = E.car(C_LIGHT, s);
         if (E.car(C_SC, s) < q.Sx && light != 0) return light > 0.;
       }
     }
   }
-  for (int s = 0; s < E.c.nC; s++) {
+  MHPPO_UNROLL
+  for (int s = 0; s < E.nC(); s++) {
     if (!in_view(E, s, mode)) continue;
     double line = E.car(C_LINE, s);
     if (is_in_front(E, q, line, 1.0)) {
@@ -335,22 +499,26 @@ MHPPO_HD inline bool choix_pedestrian(Env<V> &E, const Ped &q, int mode) {
   return true;
 }
 
-template <int V>
-MHPPO_HD inline double worst_delta_l(const Env<V> &E, const Ped &q, double pos, double spd, double line) {
+template <class EV>
+MHPPO_HD inline double worst_delta_l(const EV &E, const Ped &q, double pos, double spd, double line) {
+  constexpr int V = EV::VAR;
   if (pos > q.Sx || q.has(F_LEFT) || !is_in_front(E, q, line, 0)) return V == V_SCALABLE ? 100.0 : 0.0;
   return fabs(pos - q.Sx) - (spd * spd / (-2.0 * E.c.b00));
 }
 
-template <int V>
-MHPPO_HD inline double delta_l(const Env<V> &E, const Ped &q, double pos, double spd, double line) {
+template <class EV>
+MHPPO_HD inline double delta_l(const EV &E, const Ped &q, double pos, double spd, double line) {
+  constexpr int V = EV::VAR;
   if (pos > q.Sx || q.has(F_LEFT) || !is_in_front(E, q, line, 0)) return 0.0;
   return fabs(pos - q.Sx) - (spd * spd / (-2.0 * E.c.b00)) - 1.0 * (spd);
 }
 
-template <int V>
-MHPPO_HD inline double delta_l_all(const Env<V> &E, const Ped &q, int mode) {
+template <class EV>
+MHPPO_HD inline double delta_l_all(const EV &E, const Ped &q, int mode) {
+  constexpr int V = EV::VAR;
   double dl = V == V_SCALABLE ? 100.0 : 0.0;
-  for (int s = 0; s < E.c.nC; s++) {
+  MHPPO_UNROLL
+  for (int s = 0; s < E.nC(); s++) {
     if (!in_view(E, s, mode)) continue;
     double pos = E.car(C_SC, s), spd = E.car(C_VC, s);
     if ((pos <= q.Sx) && is_in_front(E, q, E.car(C_LINE, s), 0) && (!q.has(F_LEFT)) && (E.car(C_LIGHT, s) >= 0)) {
@@ -362,8 +530,9 @@ MHPPO_HD inline double delta_l_all(const Env<V> &E, const Ped &q, int mode) {
 }
 
 // pedestrian.get_data (:433-444); updates the running-min `delta`
-template <int V>
-MHPPO_HD inline void ped_get_data(const Env<V> &E, Ped &q, int mode, double out[9]) {
+template <class EV>
+MHPPO_HD inline void ped_get_data(const EV &E, Ped &q, int mode, double out[9]) {
+  constexpr int V = EV::VAR;
   if (!q.has(F_EXIST)) {
     for (int k = 0; k < 9; k++) out[k] = 0.;
     return;
@@ -373,8 +542,9 @@ MHPPO_HD inline void ped_get_data(const Env<V> &E, Ped &q, int mode, double out[
   out[5] = q.has(F_LEFT); out[6] = q.has(F_INCROSS); out[7] = 1.0; out[8] = (double)q.dir;
 }
 
-template <int V>
-MHPPO_HD inline double new_reward_wait_safety(const Env<V> &E, Ped &q, double spd, double pos, double line) {
+template <class EV>
+MHPPO_HD inline double new_reward_wait_safety(const EV &E, Ped &q, double spd, double pos, double line) {
+  constexpr int V = EV::VAR;
   if ((!q.has(F_LEFT)) && q.has(F_ISCROSS) && (pos < q.Sx) && is_in_front(E, q, line, 0)) {
     double exp_dl;
     if (spd < (V == V_STOP ? 0.01 : 0.05)) {  // stop :478
@@ -391,8 +561,9 @@ MHPPO_HD inline double new_reward_wait_safety(const Env<V> &E, Ped &q, double sp
 }
 
 // --------------------------------------------------------- pedestrian.step
-template <int V>
-MHPPO_HD inline void function_step(const Env<V> &E, const Ped &q, double time, double &pos, double &spd) {
+template <class EV>
+MHPPO_HD inline void function_step(const EV &E, const Ped &q, double time, double &pos, double &spd) {
+  constexpr int V = EV::VAR;
   if (q.has(F_SIN)) {
     double t = time + E.c.dt;
     double speed_p = (q.A * sin(q.W * (t - q.t0)) + q.B);
@@ -407,8 +578,9 @@ MHPPO_HD inline void function_step(const Env<V> &E, const Ped &q, double time, d
   spd = q.ivy;
 }
 
-template <int V>
-MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
+template <class EV>
+MHPPO_HD inline void ped_step(EV &E, Ped &q, double time) {
+  constexpr int V = EV::VAR;
   const double dt = E.c.dt, cl = E.cl;
   double pp_y = q.Sy + q.ivy * dt;
   {  // boolean_ped_position (:261-274)
@@ -524,9 +696,11 @@ MHPPO_HD inline void ped_step(Env<V> &E, Ped &q, double time) {
 
 // ------------------------------------------------------- pedestrian.detection
 // accumulates this ped's per-slot danger into acc[] (caller passes registers)
-template <int V, int MAXS>
-MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double *acc, bool add) {
-  const int nS = E.c.nAV;  // detection runs over the AVs (followers excluded, :845)
+template <class EV, class AV>
+MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool add) {
+  constexpr int V = EV::VAR;
+  const int nS = E.nAV();  // detection runs over the AVs (followers excluded, :845)
+  MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
     bool cond = is_in_front(E, q, E.car(C_LINE, i), 0);
     if (V == V_SCALABLE) cond = cond && (E.car(C_EXIST, i) != 0.0);
@@ -557,6 +731,7 @@ MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double
       if (Sc < q.Sx) Ts = pymax(q.wt + 10. * q.ct - tb + 1., Ts);
     } else {
       double clw = 0;
+      MHPPO_UNROLL
       for (int k = 0; k < nS; k++)
         if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0))
           clw += 1.0;
@@ -575,9 +750,11 @@ MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double
   }
   if (!add) return;
   double green = 0;
+  MHPPO_UNROLL
   for (int k = 0; k < nS; k++)
     if (E.car(C_LIGHT, k) > 0. && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0)) green += 1.0;
-  for (int i = 0; i < nS && i < MAXS; i++) {
+  MHPPO_UNROLL
+  for (int i = 0; i < nS; i++) {
     double res = E.car(C_PA, i) + E.car(C_ES, i);
     double term = 0.5 * green * (double)(E.car(C_LIGHT, i) < 0.) * (double)(E.car(C_TS, i) > 0);
     if (V == V_COOP || V == V_4CARS2 || V == V_STOP) res = res + term;
@@ -588,8 +765,9 @@ MHPPO_HD inline void ped_detection(Env<V> &E, Ped &q, const double *prev, double
 }
 
 // ---------------------------------------------------------------- car.step
-template <int V>
-MHPPO_HD inline double car_follow_action(const Env<V> &E, int s, double lead_V, double lead_S) {
+template <class EV>
+MHPPO_HD inline double car_follow_action(const EV &E, int s, double lead_V, double lead_S) {
+  constexpr int V = EV::VAR;
   double speed_car = E.car(C_VC, s);
   double diff_dist = lead_S - E.car(C_SC, s);
   double delta_v = speed_car - lead_V;
@@ -597,8 +775,9 @@ MHPPO_HD inline double car_follow_action(const Env<V> &E, int s, double lead_V, 
   return E.c.b10 * (1 - pow(speed_car / 10., 4.0) - pow(sm / diff_dist, 2.0));
 }
 
-template <int V>
-MHPPO_HD inline void car_step(const Env<V> &E, int s, double action, double light) {
+template <class EV>
+MHPPO_HD inline void car_step(const EV &E, int s, double action, double light) {
+  constexpr int V = EV::VAR;
   const double dt = E.c.dt;
   double Vc = E.car(C_VC, s);
   double acc = pymin(pymax(action, E.c.b00), E.c.b10);
@@ -624,5 +803,55 @@ MHPPO_HD inline void car_step(const Env<V> &E, int s, double action, double ligh
 }
 
 MHPPO_HD inline double car_reward(double Vc) { return -10. * pow(Vc - 10.0, 2.0) / 100.0; }
+
+
+#ifdef __HIP__  // HIP translation units (host and device passes), not the host-only simulator
+// Wave-cooperative regeneration of stale MT blocks (see RngT): for every lane of this
+// wave whose next block is stale, the 64 lanes load its active block (coalesced),
+// twist it in three dependency phases through LDS and store the next block.  Call at
+// kernel start from every lane of the wave (valid = this lane owns an env).
+template <int WAVES>
+__device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool valid) {
+  __shared__ uint32_t sh_src[WAVES][MT_N], sh_dst[WAVES][MT_N];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int mtb = valid ? b.envi[EI_MTB * N + e] : 0;
+  uint64_t stale = __ballot(valid && (mtb & 2));
+  if (!stale) return;
+  uint32_t *src = sh_src[w], *dst = sh_dst[w];
+  while (stale) {
+    const int l = __ffsll((unsigned long long)stale) - 1;
+    stale &= stale - 1;
+    const int el = __shfl(e, l), bl = __shfl(mtb, l);
+    uint32_t *blk = b.mt + (size_t)el * (MT_BLOCKS * MT_N);
+    const uint32_t *g_src = blk + (bl & 1) * MT_N;
+    uint32_t *g_dst = blk + ((bl & 1) ^ 1) * MT_N;
+    for (int k = lane; k < MT_N; k += 64) src[k] = g_src[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = lane; k < 227; k += 64) dst[k] = src[k + 397] ^ mt_mix(src[k], src[k + 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = 227 + lane; k < 454; k += 64) dst[k] = dst[k - 227] ^ mt_mix(src[k], src[k + 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = 454 + lane; k < 623; k += 64) dst[k] = dst[k - 227] ^ mt_mix(src[k], src[k + 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) dst[623] = dst[396] ^ mt_mix(src[623], dst[0]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = lane; k < MT_N; k += 64) g_dst[k] = dst[k];
+    if (lane == l) b.envi[EI_MTB * N + el] = bl & 1;
+    // the owning lane reads the new block later in this launch: stores complete first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+#endif
 
 }  // namespace mhppo

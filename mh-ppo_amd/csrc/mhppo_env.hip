@@ -21,6 +21,7 @@ constexpr int TPB = 256;
 template <int V>
 __global__ void __launch_bounds__(TPB) k_env_reset(Cfg c, Bufs b, float *obs) {
   int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(b, c.N, e, e < c.N);
   if (e < c.N) env_reset_one<V>(c, b, e, obs);
 }
 
@@ -28,9 +29,31 @@ template <int V>
 __global__ void __launch_bounds__(TPB)
     k_env_step(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
   int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(b, c.N, e, e < c.N);
   if (e < c.N)
     env_step_one<V>(c, b, e, actions + (size_t)e * 2 * c.nS, obs, rew ? rew + (size_t)e * c.nAV : nullptr,
                     rlight ? rlight + (size_t)e * c.nAV : nullptr, done);
+}
+
+template <int V, int NC, int NAV, int NP>
+__global__ void __launch_bounds__(TPB)
+    k_env_step_r(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(b, c.N, e, e < c.N);
+  if (e < c.N) {
+    constexpr int NS = V == V_4CARS2 ? 2 * NAV : NAV;
+    const double *ap = actions + (size_t)e * 2 * NS;
+    PlainArr<double, 2 * NS> act;
+#pragma unroll
+    for (int k = 0; k < 2 * NS; k++) act.v[k] = ap[k];
+    EnvR<V, NC, NAV, NP> E(c, b, e);
+    env_step_body(E, act, obs, done);
+#pragma unroll
+    for (int i = 0; i < NAV; i++) {
+      if (rew) rew[(size_t)e * NAV + i] = E.rw.v[i];
+      if (rlight) rlight[(size_t)e * NAV + i] = E.rl.v[i];
+    }
+  }
 }
 
 __global__ void __launch_bounds__(TPB) k_env_seed(Cfg c, Bufs b) {
@@ -46,7 +69,11 @@ __global__ void __launch_bounds__(TPB) k_env_state(Cfg c, Bufs b, double *out, i
 
 __global__ void k_env_rng(Cfg c, Bufs b, uint32_t *mt, int32_t *mti) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
-  if (i < (size_t)c.N * 624) mt[i] = b.mt[i];
+  // the active block of each env (the CPython state) and its cursor
+  if (i < (size_t)c.N * MT_N) {
+    const size_t e = i / MT_N, k = i % MT_N;
+    mt[i] = b.mt[e * (MT_BLOCKS * MT_N) + (b.envi[EI_MTB * c.N + e] & 1) * MT_N + k];
+  }
   if (i < (size_t)c.N) mti[i] = b.envi[EI_MTI * c.N + i];
 }
 
@@ -95,7 +122,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   size_t N = (size_t)c.N;
   size_t bytes_car = sizeof(double) * C_NF * c.nC * N, bytes_ped = sizeof(double) * P_NF * c.P * N;
   size_t bytes_pfl = sizeof(uint32_t) * c.P * N, bytes_envd = sizeof(double) * E_ND * N;
-  size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * 624 * N;
+  size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * MT_BLOCKS * MT_N * N;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_mt);
   if (hipMalloc(&h->blob, total) != hipSuccess) {
@@ -157,6 +184,16 @@ int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *re
                    uint8_t *done, void *stream) {
   if (!env || !actions) return set_error(MHPPO_EINVAL, "null env/actions");
   dim3 grid((env->c.N + TPB - 1) / TPB);
+  const Cfg &c = env->c;
+#define STEP_REG(V_, NC_, NAV_, NP_)                                                                    \
+  if (use_reg_view(c, V_, NC_, NAV_, NP_)) {                                                            \
+    hipLaunchKernelGGL((k_env_step_r<V_, NC_, NAV_, NP_>), grid, dim3(TPB), 0, (hipStream_t)stream, c, env->b, \
+                       actions, obs, rewards, reward_light, done);                                     \
+    CHECK_HIP(hipGetLastError());                                                                       \
+    return MHPPO_OK;                                                                                    \
+  }
+  MHPPO_REG_SHAPES(STEP_REG)
+#undef STEP_REG
   VARIANT_LAUNCH(k_env_step, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, actions, obs, rewards,
                  reward_light, done);
   CHECK_HIP(hipGetLastError());

@@ -111,22 +111,27 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
   B.out_c[r] = t + m.mean;
 }
 
-// one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min
-template <int V>
-__global__ void __launch_bounds__(TPB)
-    k_sample_env(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
-  int e = blockIdx.x * TPB + threadIdx.x;
-  if (e >= c.N) return;
+// one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min.
+// All of this lane's rollout inputs are read before any buffer write so the loads
+// issue as one batch; EV is the generic or the register env view.
+template <class EV>
+__device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__ eps, int t,
+                                                const mhppo_rollout_bufs &B) {
+  constexpr int V = EV::VAR;
+  const Cfg &c = E.c;
+  const int e = E.e;
   const ObsLayout L = obs_layout(c);
-  const int S = c.nS, P = c.P, T = B.T;
-  double act[2 * MAXS], rw[MAXS], rl[MAXS];
+  const int S = E.nS(), P = E.nP(), T = B.T;
+  PlainArr<double, 2 * EV::MAXAV> act;
   const float *o = B.obs + (size_t)e * L.obs_dim;
+  MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t row0 = ((size_t)e * S + i) * P;
     float loc = 2.0f;  // torch.tensor(car_b[1,0]) (:435)
     int sel = 0;
+    MHPPO_UNROLL
     for (int p = 0; p < P; p++) {
-      if (L.scalable && o[L.ped_off + p * 9 + 7] == 0.0f) continue;
+      if (V == V_SCALABLE && o[L.ped_off + p * 9 + 7] == 0.0f) continue;
       float out = B.out_c[row0 + p];
       loc = t_minimum(loc, out);
       if (out == loc) sel = p;
@@ -144,15 +149,36 @@ __global__ void __launch_bounds__(TPB)
     int cp = B.closest[(size_t)e * S + i];
     act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
   }
-  env_step_one<V>(c, eb, e, act, B.obs, rw, rl, nullptr);
+  env_step_body(E, act, B.obs, nullptr);
+  MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t bt = ((size_t)e * S + i) * T + t;
-    B.rew[bt] = rw[i];
+    B.rew[bt] = E.rw[i];
     double m = B.ep_min[(size_t)e * S + i];
-    double x = rl[i];
+    double x = E.rl[i];
     // np.minimum: NaN-propagating
     B.ep_min[(size_t)e * S + i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));
   }
+}
+
+template <int V>
+__global__ void __launch_bounds__(TPB)
+    k_sample_env(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
+  if (e >= c.N) return;
+  Env<V> E(c, eb, e);
+  sample_env_body(E, eps, t, B);
+}
+
+template <int V, int NC, int NAV, int NP>
+__global__ void __launch_bounds__(TPB)
+    k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
+  if (e >= c.N) return;
+  EnvR<V, NC, NAV, NP> E(c, eb, e);
+  sample_env_body(E, eps, t, B);
 }
 
 // -------------------------------------------------------------- evaluation
@@ -173,6 +199,7 @@ __global__ void __launch_bounds__(TPB) k_eval_step(Cfg c, Bufs eb, mhppo_mlp mc,
   for (int i = threadIdx.x; i < szd; i += blockDim.x) Wd[i] = md.packed[i];
   __syncthreads();
   const int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
   if (e >= c.N) return;
   const ObsLayout L = obs_layout(c);
   const int S = c.nS, P = c.P, N = c.N;
@@ -442,6 +469,19 @@ double *scratch(size_t n) {
 
 inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + TPB - 1) / TPB)); }
 
+// register-view rollout step for a compiled shape (4cars2 has no rollout driver)
+template <int V, int NC, int NAV, int NP>
+bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, const mhppo_rollout_bufs &B,
+                       hipStream_t s) {
+  if constexpr (V == V_4CARS2) {
+    return false;
+  } else {
+    if (!use_reg_view(c, V, NC, NAV, NP)) return false;
+    hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
+    return true;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -484,6 +524,13 @@ int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_roll
   if (!env || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
   if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
   const Cfg &c = env_cfg(env);
+#define SAMPLE_REG(V_, NC_, NAV_, NP_)                                                   \
+  if (launch_sample_reg<V_, NC_, NAV_, NP_>(c, env_bufs(env), eps, t, *bufs, (hipStream_t)stream)) { \
+    CHECK_HIP(hipGetLastError());                                                        \
+    return MHPPO_OK;                                                                     \
+  }
+  MHPPO_REG_SHAPES(SAMPLE_REG)
+#undef SAMPLE_REG
   VLAUNCH(k_sample_env, c.variant, grid_for(c.N), 0, (hipStream_t)stream, c, env_bufs(env), eps, t, *bufs);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;

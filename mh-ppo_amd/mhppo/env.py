@@ -13,6 +13,7 @@ import torch
 from . import _lib
 
 FIX_SCALABLE_LANES = 1  # MHPPO_FIX_SCALABLE_LANES
+GENERIC_STEP = 2  # MHPPO_GENERIC_STEP
 VARIANTS = {"coop": 0, "4cars": 1, "scalable": 2, "naif": 3, "4cars2": 4, "stop": 5}
 CAR_B = ((-4.0, 10.0), (2.0, 10.0))   # Coop-MH-PPO-scalable.py:1007
 PED_B = ((-0.05, 0.75, 0.0, -3.0), (0.05, 1.75, 4.0, -0.5))  # :1008
@@ -37,7 +38,7 @@ class VecCrosswalk:
 
     def __init__(self, variant, n_envs, nb_car, nb_ped, nb_lines, dt=0.3, max_episode=80,
                  simulation="sin", car_b=CAR_B, ped_b=PED_B, cross_b=CROSS_B, seed_base=0,
-                 env_id_offset=0, device=None, fix_scalable_lanes=False):
+                 env_id_offset=0, device=None, fix_scalable_lanes=False, generic_step=False):
         self.variant = variant
         self.device = torch.device(device if device is not None else "cuda")
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -58,6 +59,8 @@ class VecCrosswalk:
         cfg.seed_base = seed_base
         cfg.env_id_offset = env_id_offset
         cfg.flags = FIX_SCALABLE_LANES if fix_scalable_lanes else 0  # opt-in bug fix, SURVEY §8(f)4
+        if generic_step:  # run every step on the generic in-HBM env view (tests compare it with the register view)
+            cfg.flags |= GENERIC_STEP
         self.cfg = cfg
         self.n_envs, self.nb_car, self.nb_ped, self.nb_lines = n_envs, nb_car, nb_ped, nb_lines
         self.dt, self.max_episode = dt, max_episode

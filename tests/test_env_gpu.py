@@ -19,13 +19,17 @@ pytestmark = pytest.mark.gpu
 DISCRETE = [4, 5, 6, 7, 8, 9, 10, 11, 17, 18, 19]  # per-ped dump fields that are flags / ints
 
 
+# view "default": the register env view where compiled (single-pedestrian fixture shapes),
+# "generic": every step forced onto the in-HBM view
+@pytest.mark.parametrize("view", ["default", "generic"])
 @pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f)[4:-4] for f in FILES])
-def test_gpu_env_matches_reference(path):
+def test_gpu_env_matches_reference(path, view):
     from mhppo.env import VecCrosswalk
     g = np.load(path)
     E, T = g["obs"].shape[:2]
     npd = int(g["nb_ped"])
-    env = VecCrosswalk(str(g["variant"]), E, int(g["nb_car"]), npd, int(g["nb_lines"]), seed_base=int(g["seed_base"]))
+    env = VecCrosswalk(str(g["variant"]), E, int(g["nb_car"]), npd, int(g["nb_lines"]), seed_base=int(g["seed_base"]),
+                       generic_step=view == "generic")
     assert np.array_equal(env.reset().cpu().numpy(), g["obs0"])
     k = g["dump"].shape[2]
     for t in range(T):
@@ -70,3 +74,28 @@ def test_gpu_env_matches_oracle_many_envs(case):
         n_diff += int((r != rr).sum() + (rl != rrl).sum())
         n_tot += r.size + rl.size
     assert n_diff <= 0.2 * n_tot, f"{n_diff}/{n_tot} float64 outputs differ by more than rounding"
+
+
+@pytest.mark.parametrize("case", [("coop", 2, 1, 2), ("4cars", 4, 1, 2), ("scalable", 8, 1, 4), ("stop", 2, 1, 2),
+                                  ("4cars2", 4, 1, 2)])
+def test_register_view_is_bit_identical_to_generic(case):
+    """The register env view and the in-HBM view run the same arithmetic on the same
+    device libm: every output and the whole env state must agree bit for bit."""
+    from mhppo.env import VecCrosswalk
+    v, nc, npd, nl = case
+    N = 4096
+    envs = [VecCrosswalk(v, N, nc, npd, nl, seed_base=777, generic_step=g) for g in (False, True)]
+    o0 = [e.reset() for e in envs]
+    assert torch.equal(o0[0], o0[1])
+    S = envs[0].n_slots
+    gen = torch.Generator().manual_seed(4)
+    for t in range(160):  # two episodes: the second starts without a reset (time keeps running)
+        acc = torch.rand((N, S), generator=gen, dtype=torch.float64) * 7 - 4.5
+        light = torch.where(torch.rand((N, S), generator=gen) < 0.5, -1.0, 1.0).double()
+        a = torch.cat([acc.float().double(), light], 1).cuda()
+        outs = [e.step(a) for e in envs]
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), t
+    assert torch.equal(envs[0].get_state(), envs[1].get_state())
+    (m0, i0), (m1, i1) = envs[0].get_rng(), envs[1].get_rng()
+    assert torch.equal(m0, m1) and torch.equal(i0, i1)

@@ -26,12 +26,15 @@ def hostsim():
     return hs
 
 
+# view: the step on the register env view (where compiled: single-pedestrian fixture shapes)
+# or forced onto the generic in-HBM view (MHPPO_GENERIC_STEP)
+@pytest.mark.parametrize("view", ["default", "generic"])
 @pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f)[4:-4] for f in FILES])
-def test_device_source_matches_reference(hostsim, path):
+def test_device_source_matches_reference(hostsim, path, view):
     g = np.load(path)
     E, T = g["obs"].shape[:2]
     h = hostsim.HostVec(str(g["variant"]), E, int(g["nb_car"]), int(g["nb_ped"]), int(g["nb_lines"]),
-                        seed_base=int(g["seed_base"]))
+                        seed_base=int(g["seed_base"]), flags=2 if view == "generic" else 0)
     assert np.array_equal(h.reset(), g["obs0"])
     k = g["dump"].shape[2]
     for t in range(T):

@@ -55,14 +55,14 @@ def test_gpu_rollout_matches_reference(path):
 
 
 @pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 1, 4), ("coop", 4, 2, 2),
-                                  ("stop", 2, 2, 2)])
+                                  ("stop", 2, 2, 2), ("stop", 2, 1, 2), ("4cars", 4, 1, 2, "generic")])
 def test_gpu_rollout_matches_oracle_philox(case):
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
     from mhppo.rollout import RolloutGPU
-    v, nc, npd, nl = case
+    v, nc, npd, nl = case[:4]
     N = 256
-    venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=31000)
+    venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=31000, generic_step=len(case) > 4)
     ro = RolloutGPU(venv)
     torch.manual_seed(5)
     ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()

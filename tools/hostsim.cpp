@@ -26,7 +26,7 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   h->b.pfl = (uint32_t *)calloc((size_t)c.P * N, 4);
   h->b.envd = (double *)calloc((size_t)E_ND * N, 8);
   h->b.envi = (int32_t *)calloc((size_t)EI_NI * N, 4);
-  h->b.mt = (uint32_t *)calloc((size_t)624 * N, 4);
+  h->b.mt = (uint32_t *)calloc((size_t)MT_BLOCKS * MT_N * N, 4);
   for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
   return h;
 }
@@ -50,7 +50,18 @@ void hs_step(HostEnv *h, const double *a0, float *obs, double *rew0, double *rl0
   for (int e = 0; e < h->c.N; e++) {
     const double *a = a0 + (size_t)e * 2 * S;
     double *rew = rew0 + (size_t)e * R, *rl = rl0 + (size_t)e * R;
-    HS_DISPATCH(env_step_one<V>(h->c, h->b, e, a, obs, rew, rl, done));
+    bool reg = false;
+    // the register env view for the shapes the device compiles it for (as mhppo_env_step)
+#define HS_REG(V_, NC_, NAV_, NP_)                                       \
+    if (!reg && use_reg_view(h->c, V_, NC_, NAV_, NP_)) {                \
+      EnvR<V_, NC_, NAV_, NP_> E(h->c, h->b, e);                         \
+      env_step_body(E, a, obs, done);                                    \
+      for (int i = 0; i < R; i++) { rew[i] = E.rw[i]; rl[i] = E.rl[i]; } \
+      reg = true;                                                        \
+    }
+    MHPPO_REG_SHAPES(HS_REG)
+#undef HS_REG
+    if (!reg) HS_DISPATCH(env_step_one<V>(h->c, h->b, e, a, obs, rew, rl, done));
   }
 }
 void hs_state(HostEnv *h, double *out) {

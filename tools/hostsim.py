@@ -27,7 +27,7 @@ def _p(a):
 
 
 class HostVec:
-    def __init__(self, variant, N, nb_car, nb_ped, nb_lines, seed_base=0):
+    def __init__(self, variant, N, nb_car, nb_ped, nb_lines, seed_base=0, flags=0):
         c = _lib.EnvCfg()
         c.variant, c.n_envs, c.nb_car, c.nb_ped, c.nb_lines = VARIANTS[variant], N, nb_car, nb_ped, nb_lines
         c.max_episode, c.sin_model, c.dt = 80, 1, 0.3
@@ -37,6 +37,7 @@ class HostVec:
             c.ped_b[i] = v
         c.cross_b[0], c.cross_b[1] = CROSS_B
         c.seed_base = seed_base
+        c.flags = flags
         self.c = c
         self.h = L.hs_create(ctypes.byref(c))
         self.N = N
