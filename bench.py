@@ -163,7 +163,7 @@ def main():
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic = pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>")
-    traffic_env = pmc_traffic("k_sample_env<")
+    traffic_env = pmc_traffic("k_sample_env")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

@@ -113,8 +113,13 @@ typedef struct mhppo_mlp {
 /* Per-iteration rollout buffers for N envs, S slots, P peds, T steps (device, caller-owned).
  * Shapes: feat_d [N,S,P,dc] f32, probs_d [N,S,P,2] f32, a_d [N,S,P] i32, logp_d [N,S,P] f32,
  * closest [N,S] i32, feat_c [N,S,P,13] f32, out_c [N,S,P] f32, obs [N,obs_dim] f32 (current
- * observation), obs_c [N,S,T,13] f32, act [N,S,T] f32, logp [N,S,T] f32, rew [N,S,T] f64,
- * ep_min [N,S] f64, exist [N,S] u8. */
+ * observation), ep_min [N,S] f64, exist [N,S] u8, and the per-step records TIME-MAJOR (step t
+ * of every env is one contiguous block): obs_c [T,N,S,13] f32, act [T,N,S] f32, logp [T,N,S]
+ * f32, rew [T,N,S] f64.  The reference's episode-major batch order (:489-507) is a gather
+ * of (env, slot) segments over t, see mhppo/rollout.py bucket_segments.
+ * rows (optional, int32 [N*S*P + 2]): scratch for the head-sorted policy step — begin lists
+ * the (env, slot, ped) rows of the cross head, then those of the wait head, counts last;
+ * NULL selects the unsorted policy kernel (both are bit-identical). */
 typedef struct mhppo_rollout_bufs {
     float *feat_d, *probs_d, *logp_d;
     int32_t *a_d, *closest;
@@ -122,6 +127,7 @@ typedef struct mhppo_rollout_bufs {
     float *obs_c, *act, *logp;
     double *rew, *ep_min;
     uint8_t *exist;
+    int32_t *rows;
     int32_t T, reserved;
 } mhppo_rollout_bufs;
 
@@ -179,6 +185,9 @@ int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, 
 /* Segmented reverse discounted scan, G_t = r_t + gamma*G_{t+1} in float64, one segment of
  * T per row: rew float64 [B,T] -> ret float32 [B,T]. */
 int mhppo_returns_scan(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream);
+/* The same scan over time-major records: rew float64 [T,B] -> ret float32 [T,B] (segment b
+ * is column b; the rollout's rew buffer is [T, N*S]). */
+int mhppo_returns_scan_tm(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream);
 
 /* Advantage statistics of A = G - V over M rows: stats float64 [2] += (sum A, sum A^2)
  * (caller zeroes it; partial sums all-reduce across ranks).  Normalisation

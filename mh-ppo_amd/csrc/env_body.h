@@ -255,12 +255,14 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
       car_step(E, nS + i, a, light);
     }
   }
+  MHPPO_MARK(4);
   MHPPO_UNROLL
   for (int p = 0; p < E.nP(); p++) {
     Ped q = load_ped(E, p);
     ped_step(E, q, time);
     store_ped(E, p, q, true);
   }
+  MHPPO_MARK(5);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) acc[i] = 0.;
   MHPPO_UNROLL
@@ -270,6 +272,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     ped_detection(E, q, prev, acc, add);
     E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
   }
+  MHPPO_MARK(6);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
     E.rl[i] = acc[i];
@@ -292,11 +295,14 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     }
     E.rw[i] = r;
   }
+  MHPPO_MARK(7);
   env_observe(E, 1, obs);
+  MHPPO_MARK(8);
   int d = (time >= c.ep_len) || (E.ped_traffic() <= 0);
   if (done) done[e] = (uint8_t)d;
   b.envd[E_TIME * c.N + e] = time + c.dt;
   E.commit();
+  MHPPO_MARK(9);
 }
 
 template <int V>

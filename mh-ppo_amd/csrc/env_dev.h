@@ -33,6 +33,32 @@
 
 namespace mhppo {
 
+// Phase timing, A/B builds only (tools/ab_build.sh <name> -DMHPPO_TIMING): lane 0 of every
+// wave adds the shader-clock cycles since its previous mark to g_timing[k] (mark 0 starts
+// the clock, g_timing[15] counts waves); tools/env_phases.py reads them.  Loads are
+// asynchronous, so a phase is charged with the wait for the data it first consumes.
+#if defined(MHPPO_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+static __device__ unsigned long long g_timing[16];
+__device__ __forceinline__ void timing_mark(int k) {
+  __shared__ unsigned long long t_last[16];
+  const int w = threadIdx.x >> 6;
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long now = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  if ((threadIdx.x & 63) == 0) {
+    if (k > 0) atomicAdd(&g_timing[k], now - t_last[w]);
+    else atomicAdd(&g_timing[15], 1ull);
+    t_last[w] = now;
+  }
+}
+#define MHPPO_MARK(k) ::mhppo::timing_mark(k)
+#elif defined(MHPPO_TIMING) && defined(__HIP__)
+static __device__ unsigned long long g_timing[16];
+#define MHPPO_MARK(k)
+#else
+#define MHPPO_MARK(k)
+#endif
+
 enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP = 5 };
 // 4cars / 4cars2: nb_car AVs, each followed by an IDM car (4cars2: PPO-driven follower)
 constexpr bool has_followers(int v) { return v == V_4CARS || v == V_4CARS2; }
@@ -240,6 +266,7 @@ template <int V>
 struct Env {
   static constexpr int VAR = V;
   static constexpr int MAXAV = 16;
+  static constexpr int CNS = 0, CNP = 0;  // compile-time action slots / pedestrians: not known
   using AvArr = PlainArr<double, MAXAV>;
   AvArr rw, rl;  // step outputs per AV: reward, reward_light
   const Cfg &c;
@@ -282,6 +309,7 @@ template <int V, int NC, int NAV, int NP>
 struct EnvR {
   static constexpr int VAR = V;
   static constexpr int MAXAV = NAV;
+  static constexpr int CNS = V == V_4CARS2 ? 2 * NAV : NAV, CNP = NP;
   using AvArr = PlainArr<double, NAV>;
   AvArr rw, rl;  // step outputs per AV: reward, reward_light
   const Cfg &c;

@@ -111,6 +111,109 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
   B.out_c[r] = t + m.mean;
 }
 
+// Head-sorted policy step.  mhppo_rollout_begin lists the rows (env, slot, ped) of the
+// cross head, then those of the wait head (B.rows, counts at [R], [R+1]; the choice is
+// fixed for the episode); each wave takes 64 rows of ONE head, so the actor weights are
+// wave-uniform and stream through the scalar cache as SGPR operands of the FMAs.  (With
+// per-lane heads the weights come from LDS, and 64 lanes reading one weight cost the LDS
+// pipe 64 words: that, not the FMAs, bounds k_policy.)  Same features, same fmaf chains:
+// bit-identical to k_policy.  The waves with 64 gw < N also regenerate the stale MT19937
+// blocks of envs [64 gw, 64 gw + 64) (mt_refill_wave), off the env kernel's critical path.
+template <int V>
+__global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__restrict__ Wc,
+                                                       const float *__restrict__ Ww, float mean_c, float std_c,
+                                                       float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
+  const int lane = threadIdx.x & 63;
+  const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+  if ((int64_t)gw * 64 < c.N) mt_refill_wave<TPB / 64>(eb, c.N, gw * 64 + lane, gw * 64 + lane < c.N);
+  const int R = c.N * c.nS * c.P;
+  const int32_t *__restrict__ rows = B.rows;
+  const int nc = __builtin_amdgcn_readfirstlane(rows[R]), nw = __builtin_amdgcn_readfirstlane(rows[R + 1]);
+  const int wc = (nc + 63) / 64;
+  int head, k0, kend;
+  if (gw < wc) {
+    head = 0, k0 = gw * 64, kend = nc;
+  } else {
+    const int w2 = gw - wc;
+    if (w2 * 64 >= nw) return;
+    head = 1, k0 = nc + w2 * 64, kend = nc + nw;
+  }
+  const int k = k0 + lane;
+  if (k >= kend) return;
+  const int r = rows[k];
+  const ObsLayout L = obs_layout(c);
+  const int p = r % c.P, i = (r / c.P) % c.nS;
+  const int e = r / (c.P * c.nS);
+  const float *o = B.obs + (size_t)e * L.obs_dim;
+  float f[NF_C];
+  float ex = obs_car_ped(o, L, i, p, f);
+  float *fo = B.feat_c + (size_t)r * NF_C;
+#pragma unroll
+  for (int q = 0; q < NF_C; q++) fo[q] = f[q];
+  if (L.scalable && ex == 0.0f) return;  // `if exist:` gate of the scalable driver (:439)
+  const float out = mlp_forward13_rows(head ? Ww : Wc, f);
+  // Model_PPO type 1: tanh(x) * std + mean (:87-89), two roundings
+  const float t = tanhf(out) * (head ? std_w : std_c);
+  B.out_c[r] = t + (head ? mean_w : mean_c);
+}
+
+// Head lists for k_policy_sorted (stable: each list in row order).  Pass 1 counts the
+// cross rows of each 256-row block; pass 2 has every block sum the counts before it
+// (and all of them, for the wait list's base), then place its rows by wave prefix.
+__global__ void __launch_bounds__(TPB) k_head_count(const int32_t *a_d, int R, int32_t *cnt) {
+  __shared__ int wsum[TPB / 64];
+  const int r = blockIdx.x * TPB + threadIdx.x;
+  const bool cross = r < R && a_d[r] == 0;  // action_d = 2a - 1 <= 0 (:440-445)
+  const uint64_t m = __ballot(cross);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < TPB / 64; w++) s += wsum[w];
+    cnt[blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_head_place(const int32_t *a_d, int R, const int32_t *cnt, int nblk,
+                                                    int32_t *rows) {
+  __shared__ int red[2][TPB];
+  __shared__ int wsum[TPB / 64];
+  int before = 0, total = 0;
+  for (int b = threadIdx.x; b < nblk; b += TPB) {
+    const int v = cnt[b];
+    total += v;
+    before += b < (int)blockIdx.x ? v : 0;
+  }
+  red[0][threadIdx.x] = before;
+  red[1][threadIdx.x] = total;
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  const int nc = red[1][0], cbase = red[0][0];
+  const int r = blockIdx.x * TPB + threadIdx.x;
+  const bool valid = r < R;
+  const bool cross = valid && a_d[r] == 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t m = __ballot(cross);
+  if (lane == 0) wsum[w] = __popcll(m);
+  __syncthreads();
+  int wc = 0;
+  for (int q = 0; q < w; q++) wc += wsum[q];
+  const uint64_t below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
+  const int ci = cbase + wc + __popcll(below);                  // cross rows before r
+  const int wi = (blockIdx.x * TPB + w * 64 + lane) - ci;        // wait rows before r
+  if (valid) rows[cross ? ci : nc + wi] = r;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rows[R] = nc;
+    rows[R + 1] = R - nc;
+  }
+}
+
 // one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min.
 // All of this lane's rollout inputs are read before any buffer write so the loads
 // issue as one batch; EV is the generic or the register env view.
@@ -124,6 +227,20 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   const int S = E.nS(), P = E.nP(), T = B.T;
   PlainArr<double, 2 * EV::MAXAV> act;
   const float *o = B.obs + (size_t)e * L.obs_dim;
+  // One pedestrian and a compile-time S that is a multiple of 4: this env's selected
+  // feature rows are feat_c[e][0..S)[0] = S*13 contiguous floats on both sides, 16-B
+  // aligned (S*52 B per env), copied as float4s.
+  constexpr bool feat_rows_contiguous = EV::CNS > 0 && EV::CNS % 4 == 0 && EV::CNP == 1;
+  if constexpr (feat_rows_contiguous) {
+    constexpr int NV = EV::CNS * NF_C / 4;
+    const float4 *fs = reinterpret_cast<const float4 *>(B.feat_c + (size_t)e * (EV::CNS * NF_C));
+    float4 *fo = reinterpret_cast<float4 *>(B.obs_c + ((size_t)t * c.N + e) * (EV::CNS * NF_C));
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = fs[k];
+#pragma unroll
+    for (int k = 0; k < NV; k++) fo[k] = v[k];
+  }
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t row0 = ((size_t)e * S + i) * P;
@@ -138,27 +255,31 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     }
     float z = eps[(size_t)e * S + i];
     float a = loc + MVN_L * z;
-    size_t bt = ((size_t)e * S + i) * T + t;
+    const size_t bt = ((size_t)t * c.N + e) * S + i;  // time-major records [T][N][S]
     B.act[bt] = a;
     B.logp[bt] = mvn_logp(a, loc);
-    const float *fs = B.feat_c + (row0 + sel) * NF_C;
-    float *fo = B.obs_c + bt * NF_C;
+    if (!feat_rows_contiguous) {
+      const float *fs = B.feat_c + (row0 + sel) * NF_C;
+      float *fo = B.obs_c + bt * NF_C;
 #pragma unroll
-    for (int k = 0; k < NF_C; k++) fo[k] = fs[k];
+      for (int k = 0; k < NF_C; k++) fo[k] = fs[k];
+    }
     act[i] = (double)a;
     int cp = B.closest[(size_t)e * S + i];
     act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
   }
+  MHPPO_MARK(3);
   env_step_body(E, act, B.obs, nullptr);
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
-    size_t bt = ((size_t)e * S + i) * T + t;
+    const size_t bt = ((size_t)t * c.N + e) * S + i;
     B.rew[bt] = E.rw[i];
     double m = B.ep_min[(size_t)e * S + i];
     double x = E.rl[i];
     // np.minimum: NaN-propagating
     B.ep_min[(size_t)e * S + i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));
   }
+  MHPPO_MARK(10);
 }
 
 template <int V>
@@ -171,13 +292,18 @@ __global__ void __launch_bounds__(TPB)
   sample_env_body(E, eps, t, B);
 }
 
-template <int V, int NC, int NAV, int NP>
+// REFILL = false when k_policy_sorted ran just before (it regenerated the stale MT blocks;
+// a block still stale would be twisted in-lane by RngT, so either way the draws are exact)
+template <int V, int NC, int NAV, int NP, bool REFILL>
 __global__ void __launch_bounds__(TPB)
     k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
   int e = blockIdx.x * TPB + threadIdx.x;
-  mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
+  MHPPO_MARK(0);
+  if (REFILL) mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
+  MHPPO_MARK(1);
   if (e >= c.N) return;
   EnvR<V, NC, NAV, NP> E(c, eb, e);
+  MHPPO_MARK(2);
   sample_env_body(E, eps, t, B);
 }
 
@@ -301,6 +427,17 @@ __global__ void __launch_bounds__(TPB) k_returns(const double *rew, float *ret, 
   for (int t = T - 1; t >= 0; t--) {
     g = r[t] + gamma * g;
     o[t] = (float)g;
+  }
+}
+
+// time-major records [T][B]: lane b scans column b (coalesced across the wave)
+__global__ void __launch_bounds__(TPB) k_returns_tm(const double *rew, float *ret, int64_t B, int T, double gamma) {
+  int64_t b = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (b >= B) return;
+  double g = 0.0;
+  for (int t = T - 1; t >= 0; t--) {
+    g = rew[(int64_t)t * B + b] + gamma * g;
+    ret[(int64_t)t * B + b] = (float)g;
   }
 }
 
@@ -477,7 +614,10 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
     return false;
   } else {
     if (!use_reg_view(c, V, NC, NAV, NP)) return false;
-    hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
+    if (B.rows)
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
+    else
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
     return true;
   }
 }
@@ -485,6 +625,17 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
 }  // namespace
 
 extern "C" {
+
+#ifdef MHPPO_TIMING
+// A/B timing builds only (not part of include/mhppo.h): copy out and clear g_timing
+int mhppo_debug_timing(unsigned long long *out16) {
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)));
+  return MHPPO_OK;
+}
+#endif
 
 int mhppo_choice_dim(const mhppo_env *env) { return env ? choice_dim(env_cfg(env)) : MHPPO_EINVAL; }
 
@@ -501,6 +652,13 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
   size_t R = (size_t)c.N * c.nS * c.P;
   size_t shm = sizeof(float) * mlp_size(actor_choice->n_in, 2);
   VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, *actor_choice, u, forced_a, *bufs);
+  if (bufs->rows) {  // head lists for k_policy_sorted (the choice is fixed for the episode)
+    const int nblk = (int)grid_for(R).x;
+    int32_t *cnt = reinterpret_cast<int32_t *>(scratch((nblk + 1) / 2));
+    if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+    hipLaunchKernelGGL(k_head_count, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt);
+    hipLaunchKernelGGL(k_head_place, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt, nblk, bufs->rows);
+  }
   size_t NS = (size_t)c.N * c.nS;
   hipLaunchKernelGGL(k_fill_f64, grid_for(NS), dim3(TPB), 0, s, bufs->ep_min, NS, 0.0);  // np.array([0.]*S) (:383)
   CHECK_HIP(hipGetLastError());
@@ -514,6 +672,16 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
     return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
   const Cfg &c = env_cfg(env);
   size_t R = (size_t)c.N * c.nS * c.P;
+  if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
+  if (bufs->rows) {
+    // one wave per 64 rows of one head: at most R/64 + 2 waves, and at least N/64 (MT refill)
+    const size_t waves = (R + 63) / 64 + 2;
+    const dim3 grid((unsigned)((waves + TPB / 64 - 1) / (TPB / 64)));
+    VLAUNCH(k_policy_sorted, c.variant, grid, 0, (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed,
+            actor_cross->mean, actor_cross->std, actor_wait->mean, actor_wait->std, *bufs, env_bufs(env));
+    CHECK_HIP(hipGetLastError());
+    return MHPPO_OK;
+  }
   size_t shm = 2 * sizeof(float) * mlp_size(NF_C, 1);
   VLAUNCH(k_policy, c.variant, grid_for(R), shm, (hipStream_t)stream, c, *actor_cross, *actor_wait, *bufs);
   CHECK_HIP(hipGetLastError());
@@ -580,6 +748,14 @@ int mhppo_returns_scan(const double *rew, float *ret, int64_t B, int32_t T, doub
   if (!rew || !ret || B < 0 || T <= 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (B == 0) return MHPPO_OK;
   hipLaunchKernelGGL(k_returns, grid_for(B), dim3(TPB), 0, (hipStream_t)stream, rew, ret, B, T, gamma);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_returns_scan_tm(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream) {
+  if (!rew || !ret || B < 0 || T <= 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (B == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_returns_tm, grid_for(B), dim3(TPB), 0, (hipStream_t)stream, rew, ret, B, T, gamma);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

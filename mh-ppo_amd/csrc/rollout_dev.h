@@ -218,6 +218,40 @@ MHPPO_HD inline void mlp_forward(const float *W, int n_in, const float *x, float
   }
 }
 
+// The same arithmetic (every output's fmaf chain in the same ascending order, bias
+// last) with the loops output-major, so each output reads its weights contiguously:
+// with a wave-uniform W they stream through the scalar cache as SGPR operands.
+// Hidden 2 is kept whole (64 registers) before layer 3.
+MHPPO_HD inline float mlp_forward13_rows(const float *__restrict__ W, const float *x) {
+  constexpr int NIN = NF_C;
+  const float *w1 = W, *b1 = w1 + 32 * NIN, *w2 = b1 + 32, *b2 = w2 + 64 * 32, *w3 = b2 + 64, *b3 = w3 + 32 * 64,
+              *w4 = b3 + 32, *b4 = w4 + 32;
+  float h1[32], h2[64];
+#pragma unroll
+  for (int o = 0; o < 32; o++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NIN; k++) acc = fmaf(w1[o * NIN + k], x[k], acc);
+    h1[o] = relu(acc + b1[o]);
+  }
+#pragma unroll
+  for (int o2 = 0; o2 < 64; o2++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 32; k++) acc = fmaf(w2[o2 * 32 + k], h1[k], acc);
+    h2[o2] = relu(acc + b2[o2]);
+  }
+  float y = 0.0f;
+#pragma unroll
+  for (int o = 0; o < 32; o++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) acc = fmaf(w3[o * 64 + k], h2[k], acc);
+    y = fmaf(w4[o], relu(acc + b3[o]), y);
+  }
+  return y + b4[0];
+}
+
 // MVN(loc, diag(0.5)) in float32, the arithmetic torch performs
 // (multivariate_normal.py rsample/log_prob; pinned in tests/test_rollout_math.py):
 //   sample a = loc + L*eps;  x = (a - loc) * (1/L);  logp = -0.5*(log(2 pi) + x*x) - log(L)

@@ -35,7 +35,8 @@ class Mlp(ctypes.Structure):
 class RolloutBufs(ctypes.Structure):
     _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
                 ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
-                ("rew", P), ("ep_min", P), ("exist", P), ("T", I32), ("reserved", I32)]
+                ("rew", P), ("ep_min", P), ("exist", P), ("rows", P), ("T", I32),
+                ("reserved", I32)]
 
 
 class EvalBufs(ctypes.Structure):
@@ -69,6 +70,7 @@ _SIGS = {
     "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
     "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),
+    "mhppo_returns_scan_tm": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_adv_stats": (I32, [P, P, I64, P, P]),
     "mhppo_adv_normalize": (I32, [P, P, I64, P, F64, P, P]),
     "mhppo_ppo_cont_fwd_bwd": (I32, [P, P, P, P, I64, F64, P, P, P]),

@@ -4,9 +4,11 @@ Batched form of `Env_rollout.iterations_rand` (Coop-MH-PPO-scalable.py:357-517;
 coop driver Coop-MH-PPO.ipynb cell 0): every env plays one 80-step episode;
 the choice head is sampled once at t=0 (ped_traffic never changes, so
 `need_new_d` is only true at the start); each step runs the fused
-policy kernel and the fused sample+env-step kernel.  Buffers are laid out
-[env, slot, t], which is exactly the reference's episode-major, car-major,
-time-ascending batch order once segments are bucketed (bucket_segments).
+policy kernel and the fused sample+env-step kernel.  The per-step records are
+written time-major, [t, env, slot] (each step's writes are one contiguous block
+in HBM); RolloutBatch exposes them as [env, slot, t] views, and bucket_segments
+gathers (env, slot) segments over t into the reference's episode-major,
+car-major, time-ascending batch order.
 
 Noise: in perf mode the standard normals (MVN eps) and the Categorical
 uniforms come from Philox keyed by (seed, iteration) with counters built from
@@ -51,17 +53,19 @@ class RolloutGPU:
         self.feat_c = z((N, S, P, NF_C), f32)
         self.out_c = z((N, S, P), f32)
         self.obs = z((N, venv.obs_dim), f32)
-        self.obs_c = z((N, S, self.T, NF_C), f32)
-        self.act = z((N, S, self.T), f32)
-        self.logp = z((N, S, self.T), f32)
-        self.rew = z((N, S, self.T), f64)
+        # time-major records [T, N, S(, 13)] (include/mhppo.h mhppo_rollout_bufs)
+        self.obs_c = z((self.T, N, S, NF_C), f32)
+        self.act = z((self.T, N, S), f32)
+        self.logp = z((self.T, N, S), f32)
+        self.rew = z((self.T, N, S), f64)
         self.ep_min = z((N, S), f64)
         self.exist = z((N, S), torch.uint8)
         self.eps = z((self.T, N, S), f32)
         self.u = z((N, S, P), f32)
+        self.rows = z(N * S * P + 2, i32)  # head-sorted policy rows (filled by mhppo_rollout_begin)
         b = _lib.RolloutBufs()
         for name in ("feat_d", "probs_d", "logp_d", "a_d", "closest", "feat_c", "out_c", "obs", "obs_c", "act",
-                     "logp", "rew", "ep_min", "exist"):
+                     "logp", "rew", "ep_min", "exist", "rows"):
             setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
         b.T = self.T
         self._bufs = b
@@ -142,9 +146,23 @@ class RolloutGPU:
             if step_events is not None:
                 step_events[t][1].record()
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
+        # obs_c/act/logp/rew: [N, S, T(, 13)] views of the time-major buffers (*_tm)
         return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,
-                            closest=self.closest, obs_c=self.obs_c, act=self.act, logp=self.logp, rew=self.rew,
-                            ep_min=self.ep_min, exist=self.exist, N=self.N, S=self.S, P=self.P, T=self.T)
+                            closest=self.closest, obs_c=self.obs_c.permute(1, 2, 0, 3), act=self.act.permute(1, 2, 0),
+                            logp=self.logp.permute(1, 2, 0), rew=self.rew.permute(1, 2, 0), obs_c_tm=self.obs_c,
+                            act_tm=self.act, logp_tm=self.logp, rew_tm=self.rew, ep_min=self.ep_min,
+                            exist=self.exist, N=self.N, S=self.S, P=self.P, T=self.T)
+
+
+def returns_scan_tm(rew_tm, gamma=0.99):
+    """futur_rewards over time-major records: rew float64 [T, ...] (one segment per column)
+    -> float32 [T, ...]."""
+    T = rew_tm.shape[0]
+    r = rew_tm.reshape(T, -1).contiguous()
+    out = torch.empty(r.shape, dtype=torch.float32, device=rew_tm.device)
+    _lib.check(_lib.lib().mhppo_returns_scan_tm(_lib.ptr(r), _lib.ptr(out), r.shape[1], T, gamma,
+                                                _lib.stream_ptr()))
+    return out.reshape(rew_tm.shape)
 
 
 def returns_scan(rew, gamma=0.99):
@@ -179,14 +197,17 @@ def bucket_segments(batch, fix_bucket=False):
     seg_cross = torch.nonzero(cross.reshape(-1)).squeeze(1)
     seg_wait = torch.nonzero(wait.reshape(-1)).squeeze(1)
     seg_all = torch.nonzero(exist.reshape(-1)).squeeze(1)
-    ret = returns_scan(batch.rew)
+    ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
+    t_off = torch.arange(T, device=seg_all.device, dtype=torch.int64) * (N * S)
 
     def rows(seg):
-        obs = batch.obs_c.reshape(N * S, T, NF_C).index_select(0, seg).reshape(-1, NF_C)
-        act = batch.act.reshape(N * S, T).index_select(0, seg).reshape(-1)
-        lp = batch.logp.reshape(N * S, T).index_select(0, seg).reshape(-1)
-        rt = ret.reshape(N * S, T).index_select(0, seg).reshape(-1)
-        rw = batch.rew.reshape(N * S, T).index_select(0, seg).reshape(-1)
+        # row (segment k, step t) of the bucket = record t * N*S + seg[k]: segment-major order
+        idx = (seg.unsqueeze(1) + t_off.unsqueeze(0)).reshape(-1)
+        obs = batch.obs_c_tm.reshape(T * N * S, NF_C).index_select(0, idx)
+        act = batch.act_tm.reshape(-1).index_select(0, idx)
+        lp = batch.logp_tm.reshape(-1).index_select(0, idx)
+        rt = ret.reshape(-1).index_select(0, idx)
+        rw = batch.rew_tm.reshape(-1).index_select(0, idx)
         return dict(obs=obs, act=act, logp=lp, ret=rt, rew=rw, n_seg=int(seg.numel()))
 
     cl = batch.closest.reshape(N * S).long().index_select(0, seg_all)

@@ -65,6 +65,17 @@ def test_returns_scan_bit_exact():
     assert torch.equal(out, ref)
 
 
+def test_returns_scan_time_major_bit_exact():
+    """The rollout's time-major records [T, N, S]: column scan == the oracle's row scan."""
+    from mhppo.rollout import returns_scan_tm
+    from oracle import ppo_ref
+    rng = np.random.default_rng(1)
+    rew = torch.tensor(rng.normal(-10, 5, size=(777, 80)))
+    ref = ppo_ref.returns_scan(rew)
+    out = returns_scan_tm(rew.t().contiguous().reshape(80, 7, 111).cuda()).cpu().reshape(80, 777).t()
+    assert torch.equal(out, ref)
+
+
 def test_philox_noise_moments():
     from mhppo import _lib
     n = 1 << 20
