@@ -39,13 +39,16 @@ F32_MFMA_PEAK_TFLOPS = 157.3
 
 
 def env_step_bytes(S, nC, P, obs_dim, T=80):
-    """Algorithmic HBM bytes one env moves in one fused sample+env-step launch."""
+    """Algorithmic HBM bytes one env moves in one fused sample+env-step launch.
+    With one pedestrian the policy kernel writes the step's feature record in place
+    (include/mhppo.h), so this kernel neither reads feat_c nor writes obs_c."""
     car = nC * 11 * 8 + nC * 6 * 8 + S * 3 * 8      # read 11 fields/car, write 6 dynamic (+3 detection fields per AV)
     ped = P * (17 * 8 + 4) + P * (10 * 8 + 4)      # read 17 f64 + flags, write 10 dynamic f64 + flags
-    env = 8 + 8 + 4 + 4 + 4 + 8                   # cross, time r/w, mti r/w, ped_traffic, RNG words
-    io_in = S * P * 4 + S * 13 * 4 + S * 4 + S * P * 4 + S * 4 + S * 8   # out_c, feat_c(sel), eps, a_d, closest, ep_min
-    io_out = S * 13 * 4 + S * 4 + S * 4 + S * 8 + S * 8 + obs_dim * 4     # obs_c, act, logp, rew, ep_min, obs
-    return car + ped + env + io_in + io_out
+    env = 8 + 8 + 4 + 4 + 4 + 4 + 8               # cross, time r/w, mti r/w, block bits, ped_traffic, RNG words
+    feat = 0 if P == 1 else 2 * S * 13 * 4          # selected feature row: read feat_c, write obs_c
+    io_in = S * P * 4 + S * 4 + S * P * 4 + S * 4 + S * 8   # out_c, eps, a_d, closest, ep_min
+    io_out = S * 4 + S * 4 + S * 8 + S * 8 + obs_dim * 4     # act, logp, rew, ep_min, obs
+    return car + ped + env + feat + io_in + io_out
 
 
 def pmc_traffic(*patterns):

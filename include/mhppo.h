@@ -117,6 +117,8 @@ typedef struct mhppo_mlp {
  * of every env is one contiguous block): obs_c [T,N,S,13] f32, act [T,N,S] f32, logp [T,N,S]
  * f32, rew [T,N,S] f64.  The reference's episode-major batch order (:489-507) is a gather
  * of (env, slot) segments over t, see mhppo/rollout.py bucket_segments.
+ * With P == 1, feat_c may point at obs_c + t*N*S*13 for step t (the selected feature row is
+ * the only row, so the policy writes the record in place and sample_env copies nothing).
  * rows (optional, int32 [N*S*P + 2]): scratch for the head-sorted policy step — begin lists
  * the (env, slot, ped) rows of the cross head, then those of the wait head, counts last;
  * NULL selects the unsorted policy kernel (both are bit-identical). */

@@ -162,7 +162,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   Env<V> E(c, b, e);
   E.cross = E.rng.uniform(c.xb0, c.xb1);
   E.cl = (double)c.nb_lines * E.cross;
-  b.envd[E_CROSS * c.N + e] = E.cross;
+  b.envd[sidx(E_ND, E_CROSS, e)] = E.cross;
   for (int p = 0; p < c.P; p++) {
     Ped q;
     ped_init(E, q, 0, 0);
@@ -196,9 +196,9 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
     if (has_followers(V))
       for (int i = 0; i < c.nb_car; i++) car_init(E, c.nAV + i, E.car(C_LINE, i), 0, 1);
   }
-  b.envi[EI_CARTRAF * c.N + e] = car_traffic;
+  b.envi[sidx(EI_NI, EI_CARTRAF, e)] = car_traffic;
   int ped_traffic = E.rng.randint(1, c.nb_ped);
-  b.envi[EI_PEDTRAF * c.N + e] = ped_traffic;
+  b.envi[sidx(EI_NI, EI_PEDTRAF, e)] = ped_traffic;
   for (int p = 0; p < ped_traffic; p++) {
     Ped q;
     ped_init(E, q, 1, 1);
@@ -214,7 +214,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
     }
   }
   env_observe(E, 0, obs);
-  b.envd[E_TIME * c.N + e] = 0.0;
+  b.envd[sidx(E_ND, E_TIME, e)] = 0.0;
   E.save_rng();
 }
 
@@ -228,7 +228,8 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
   const Bufs &b = E.b;
   const int e = E.e;
   const int nS = E.nAV();  // AV slots (4cars2: followers handled below)
-  double time = b.envd[E_TIME * c.N + e];
+  double time = b.envd[sidx(E_ND, E_TIME, e)];
+  E.rng.prefetch();  // register view: the draws' window, in flight during the car steps
   typename EV::AvArr prev, acc;
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) prev[i] = E.car(C_SC, i);
@@ -300,7 +301,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
   MHPPO_MARK(8);
   int d = (time >= c.ep_len) || (E.ped_traffic() <= 0);
   if (done) done[e] = (uint8_t)d;
-  b.envd[E_TIME * c.N + e] = time + c.dt;
+  b.envd[sidx(E_ND, E_TIME, e)] = time + c.dt;
   E.commit();
   MHPPO_MARK(9);
 }
@@ -322,10 +323,10 @@ MHPPO_HD inline void env_seed_one(const Cfg &c, const Bufs &b, int e) {
   uint32_t *blk = b.mt + (size_t)e * (MT_BLOCKS * MT_N);
   rng_seed(blk, c.seed_base + c.env_off + (uint64_t)e);
   mt_twist_into(blk, blk + MT_N);  // next block ready: active 0, not stale
-  b.envi[EI_MTI * c.N + e] = MT_N;
-  b.envi[EI_MTB * c.N + e] = 0;
-  b.envd[E_CROSS * c.N + e] = 0.0;
-  b.envd[E_TIME * c.N + e] = 0.0;
+  b.envi[sidx(EI_NI, EI_MTI, e)] = MT_N;
+  b.envi[sidx(EI_NI, EI_MTB, e)] = 0;
+  b.envd[sidx(E_ND, E_CROSS, e)] = 0.0;
+  b.envd[sidx(E_ND, E_TIME, e)] = 0.0;
 }
 
 // ------------------------------------------------------------- state dump
@@ -349,9 +350,9 @@ MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int
     for (int j = 0; j < 8; j++) o[k++] = f[j];
   }
   o[k++] = E.cross;
-  o[k++] = b.envd[E_TIME * c.N + e];
-  o[k++] = (double)b.envi[EI_PEDTRAF * c.N + e];
-  o[k++] = (double)b.envi[EI_CARTRAF * c.N + e];
+  o[k++] = b.envd[sidx(E_ND, E_TIME, e)];
+  o[k++] = (double)b.envi[sidx(EI_NI, EI_PEDTRAF, e)];
+  o[k++] = (double)b.envi[sidx(EI_NI, EI_CARTRAF, e)];
   for (int p = 0; p < c.P; p++) o[k++] = (E.pflag(p) & F_EXIST) ? 1.0 : 0.0;
 }
 

@@ -1,8 +1,8 @@
 // env_dev.h — device-side crosswalk env for gfx950: one env per lane.
 //
-// State lives in HBM as structure-of-arrays, field-major with the env index
-// fastest ([field][slot][N]), so every per-lane access of a wave is one
-// coalesced 512-B transaction.  Each env draws from its own CPython-compatible
+// State lives in HBM as structure-of-arrays blocked by 64 envs ([N/64][field][slot][64],
+// sidx), so every per-lane access of a wave is one coalesced 512-B transaction and a
+// wave's whole state is one contiguous block.  Each env draws from its own CPython-compatible
 // MT19937 stream (two blocks [N][2][624] u32 + cursor), so trajectories are the
 // reference's on `random.seed(seed_base + env_id)` and invariant to how envs
 // are sharded over GPUs.
@@ -63,12 +63,12 @@ enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP
 // 4cars / 4cars2: nb_car AVs, each followed by an IDM car (4cars2: PPO-driven follower)
 constexpr bool has_followers(int v) { return v == V_4CARS || v == V_4CARS2; }
 
-// car fields (double) [C_NF][nC][N]
+// car fields (double) [C_NF][nC] per env (env-blocked, see sidx)
 enum { C_AC, C_VC, C_SC, C_LIGHT, C_PA, C_ES, C_TS, C_H0, C_H1, C_LINE, C_EXIST, C_NF };
-// ped fields (double) [P_NF][P][N]
+// ped fields (double) [P_NF][P] per env
 enum { P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS, P_IVX, P_IVY, P_RATIO,
        P_CSTOP, P_A, P_B, P_W, P_NF };
-// ped flag word bits [P][N] (u32)
+// ped flag word bits [P] per env (u32)
 enum : uint32_t {
   F_DECISION = 1u << 0, F_ATCROSS = 1u << 1, F_LEFT = 1u << 2, F_INCROSS = 1u << 3,
   F_ACCIDENT = 1u << 4, F_STOP = 1u << 5, F_WSA = 1u << 6, F_NEEDSTOP = 1u << 7,
@@ -93,13 +93,23 @@ struct Cfg {
 };
 
 struct Bufs {
-  double *car;    // [C_NF][nC][N]
-  double *ped;    // [P_NF][P][N]
-  uint32_t *pfl;  // [P][N]
-  double *envd;   // [E_ND][N]
-  int32_t *envi;  // [EI_NI][N]
+  double *car;    // [N/EB][C_NF][nC][EB]  (env-blocked: index with sidx)
+  double *ped;    // [N/EB][P_NF][P][EB]
+  uint32_t *pfl;  // [N/EB][P][EB]
+  double *envd;   // [N/EB][E_ND][EB]
+  int32_t *envi;  // [N/EB][EI_NI][EB]
   uint32_t *mt;   // [N][2][624] (active + next block, see RngT)
 };
+
+// Env-blocked state layout: every field array ([rows] per env: car C_NF*nC, ped P_NF*P,
+// flags P, envd E_ND, envi EI_NI) is stored [ceil(N/EB)][rows][EB], so one wave's 64 envs
+// own one contiguous block (a few KB) instead of rows 8*N bytes apart: the same 512-B
+// coalesced access per field, but a wave's state load touches one DRAM/TLB region.
+constexpr int EB = 64;
+MHPPO_HD __forceinline__ size_t sidx(int rows, int row, int e) {
+  return ((size_t)(e >> 6) * (size_t)rows + (size_t)row) * EB + (size_t)(e & (EB - 1));
+}
+MHPPO_HD __forceinline__ size_t npad(int N) { return ((size_t)N + EB - 1) / EB * EB; }
 
 MHPPO_HD __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
 MHPPO_HD __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
@@ -115,7 +125,7 @@ static constexpr double NV_MAGICCONST = 0x1.b72cd3f331398p+0;  // 4*exp(-0.5)/sq
 // the start of the next env kernel (mt_refill_wave: coalesced loads, three LDS
 // phases, coalesced stores), so the 624-step twist never sits on one lane's
 // critical path.  envi[EI_MTB]: bit 0 = active block, bit 1 = the other block is stale.
-enum : int { MT_N = 624, MT_BLOCKS = 2 };
+enum : int { MT_N = 624, MT_BLOCKS = 2, MT_PAD = 64 };  // MT_PAD: words after the last env's blocks
 
 MHPPO_HD inline uint32_t mt_mix(uint32_t a, uint32_t b) {  // one twist term of (a, successor b)
   uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -151,7 +161,9 @@ struct RngT {
     if (K == 0) return;
     nwin = (MT_N - mti) < K ? (MT_N - mti) : K;
 #pragma unroll
-    for (int k = 0; k < (K > 0 ? K : 1); k++) win[k] = (k < nwin) ? mt[mti + k] : 0u;
+    // unconditional loads (one batch, no branches): words past the active block read the
+    // next block or the allocation's tail padding (MT_PAD) and are never consumed
+    for (int k = 0; k < (K > 0 ? K : 1); k++) win[k] = mt[mti + k];
   }
   MHPPO_HD uint32_t genrand() {
     if (mti >= MT_N) {
@@ -276,25 +288,25 @@ struct Env {
   double cross, cl;  // crosswalk lane width, cross_lines = nb_lines * cross
 
   MHPPO_HD Env(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
-    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[EI_MTI * c.N + e], b.envi[EI_MTB * c.N + e]);
-    cross = b.envd[E_CROSS * c.N + e];
+    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[sidx(EI_NI, EI_MTI, e)], b.envi[sidx(EI_NI, EI_MTB, e)]);
+    cross = b.envd[sidx(E_ND, E_CROSS, e)];
     cl = (double)c.nb_lines * cross;
   }
   MHPPO_HD void save_rng() {
-    b.envi[EI_MTI * c.N + e] = rng.mti;
-    b.envi[EI_MTB * c.N + e] = rng.mtb;
+    b.envi[sidx(EI_NI, EI_MTI, e)] = rng.mti;
+    b.envi[sidx(EI_NI, EI_MTB, e)] = rng.mtb;
   }
   MHPPO_HD void commit() { save_rng(); }
   MHPPO_HD int nC() const { return c.nC; }
   MHPPO_HD int nAV() const { return c.nAV; }
   MHPPO_HD int nS() const { return c.nS; }
   MHPPO_HD int nP() const { return c.P; }
-  MHPPO_HD int ped_traffic() const { return b.envi[EI_PEDTRAF * c.N + e]; }
-  MHPPO_HD int car_traffic() const { return b.envi[EI_CARTRAF * c.N + e]; }
+  MHPPO_HD int ped_traffic() const { return b.envi[sidx(EI_NI, EI_PEDTRAF, e)]; }
+  MHPPO_HD int car_traffic() const { return b.envi[sidx(EI_NI, EI_CARTRAF, e)]; }
 
-  MHPPO_HD double &car(int f, int s) const { return b.car[((size_t)f * c.nC + s) * c.N + e]; }
-  MHPPO_HD double &pedf(int f, int p) const { return b.ped[((size_t)f * c.P + p) * c.N + e]; }
-  MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[(size_t)p * c.N + e]; }
+  MHPPO_HD double &car(int f, int s) const { return b.car[sidx(C_NF * c.nC, f * c.nC + s, e)]; }
+  MHPPO_HD double &pedf(int f, int p) const { return b.ped[sidx(P_NF * c.P, f * c.P + p, e)]; }
+  MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[sidx(c.P, p, e)]; }
 };
 
 // EnvR<V, NC, NAV, NP>: compile-time shape (NC car slots, NAV AVs, NP pedestrians).
@@ -324,22 +336,23 @@ struct EnvR {
 
   MHPPO_HD EnvR(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
     const size_t N = (size_t)c.N;
-    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[EI_MTI * N + e], b.envi[EI_MTB * N + e]);
-    cross = b.envd[E_CROSS * N + e];
+    rng.attach(b.mt + (size_t)e * (MT_BLOCKS * MT_N), b.envi[sidx(EI_NI, EI_MTI, e)], b.envi[sidx(EI_NI, EI_MTB, e)]);
+    cross = b.envd[sidx(E_ND, E_CROSS, e)];
     cl = (double)c.nb_lines * cross;
-    ptraf = b.envi[EI_PEDTRAF * N + e];
-    ctraf = b.envi[EI_CARTRAF * N + e];
+    ptraf = b.envi[sidx(EI_NI, EI_PEDTRAF, e)];
+    ctraf = b.envi[sidx(EI_NI, EI_CARTRAF, e)];
 #pragma unroll
     for (int f = 0; f < C_NF; f++)
 #pragma unroll
-      for (int s = 0; s < NC; s++) car_[f][s] = b.car[((size_t)f * NC + s) * N + e];
+      for (int s = 0; s < NC; s++) car_[f][s] = b.car[sidx(C_NF * NC, f * NC + s, e)];
 #pragma unroll
     for (int f = 0; f < P_NF; f++)
 #pragma unroll
-      for (int p = 0; p < NP; p++) ped_[f][p] = b.ped[((size_t)f * NP + p) * N + e];
+      for (int p = 0; p < NP; p++) ped_[f][p] = b.ped[sidx(P_NF * NP, f * NP + p, e)];
 #pragma unroll
-    for (int p = 0; p < NP; p++) pfl_[p] = b.pfl[(size_t)p * N + e];
-    rng.prefetch();
+    for (int p = 0; p < NP; p++) pfl_[p] = b.pfl[sidx(NP, p, e)];
+    // the RNG window is fetched at the start of the step (env_step_body): its address
+    // depends on the cursor loaded here, and the car steps cover the round trip
   }
   // dynamic fields only: line/exist and the pedestrian's static draws never change in a step
   MHPPO_HD void commit() {
@@ -350,19 +363,19 @@ struct EnvR {
 #pragma unroll
     for (int k = 0; k < 6; k++)
 #pragma unroll
-      for (int s = 0; s < NC; s++) b.car[((size_t)dyn_car[k] * NC + s) * N + e] = car_[dyn_car[k]][s];
+      for (int s = 0; s < NC; s++) b.car[sidx(C_NF * NC, dyn_car[k] * NC + s, e)] = car_[dyn_car[k]][s];
 #pragma unroll
     for (int k = 0; k < 3; k++)
 #pragma unroll
-      for (int s = 0; s < NAV; s++) b.car[((size_t)det_car[k] * NC + s) * N + e] = car_[det_car[k]][s];
+      for (int s = 0; s < NAV; s++) b.car[sidx(C_NF * NC, det_car[k] * NC + s, e)] = car_[det_car[k]][s];
 #pragma unroll
     for (int k = 0; k < 10; k++)
 #pragma unroll
-      for (int p = 0; p < NP; p++) b.ped[((size_t)dyn_ped[k] * NP + p) * N + e] = ped_[dyn_ped[k]][p];
+      for (int p = 0; p < NP; p++) b.ped[sidx(P_NF * NP, dyn_ped[k] * NP + p, e)] = ped_[dyn_ped[k]][p];
 #pragma unroll
-    for (int p = 0; p < NP; p++) b.pfl[(size_t)p * N + e] = pfl_[p];
-    b.envi[EI_MTI * N + e] = rng.mti;
-    b.envi[EI_MTB * N + e] = rng.mtb;
+    for (int p = 0; p < NP; p++) b.pfl[sidx(NP, p, e)] = pfl_[p];
+    b.envi[sidx(EI_NI, EI_MTI, e)] = rng.mti;
+    b.envi[sidx(EI_NI, EI_MTB, e)] = rng.mtb;
   }
   static constexpr int nC() { return NC; }
   static constexpr int nAV() { return NAV; }
@@ -842,7 +855,7 @@ template <int WAVES>
 __device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool valid) {
   __shared__ uint32_t sh_src[WAVES][MT_N], sh_dst[WAVES][MT_N];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int mtb = valid ? b.envi[EI_MTB * N + e] : 0;
+  const int mtb = valid ? b.envi[sidx(EI_NI, EI_MTB, e)] : 0;
   uint64_t stale = __ballot(valid && (mtb & 2));
   if (!stale) return;
   uint32_t *src = sh_src[w], *dst = sh_dst[w];
@@ -874,7 +887,7 @@ __device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int k = lane; k < MT_N; k += 64) g_dst[k] = dst[k];
-    if (lane == l) b.envi[EI_MTB * N + el] = bl & 1;
+    if (lane == l) b.envi[sidx(EI_NI, EI_MTB, el)] = bl & 1;
     // the owning lane reads the new block later in this launch: stores complete first
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

@@ -72,9 +72,9 @@ __global__ void k_env_rng(Cfg c, Bufs b, uint32_t *mt, int32_t *mti) {
   // the active block of each env (the CPython state) and its cursor
   if (i < (size_t)c.N * MT_N) {
     const size_t e = i / MT_N, k = i % MT_N;
-    mt[i] = b.mt[e * (MT_BLOCKS * MT_N) + (b.envi[EI_MTB * c.N + e] & 1) * MT_N + k];
+    mt[i] = b.mt[e * (MT_BLOCKS * MT_N) + (b.envi[sidx(EI_NI, EI_MTB, e)] & 1) * MT_N + k];
   }
-  if (i < (size_t)c.N) mti[i] = b.envi[EI_MTI * c.N + i];
+  if (i < (size_t)c.N) mti[i] = b.envi[sidx(EI_NI, EI_MTI, i)];
 }
 
 }  // namespace
@@ -119,10 +119,10 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   build_cfg(*cfg, h->c);
   const Cfg &c = h->c;
   h->device = device;
-  size_t N = (size_t)c.N;
+  size_t N = npad(c.N);  // env-blocked arrays: whole blocks of EB envs
   size_t bytes_car = sizeof(double) * C_NF * c.nC * N, bytes_ped = sizeof(double) * P_NF * c.P * N;
   size_t bytes_pfl = sizeof(uint32_t) * c.P * N, bytes_envd = sizeof(double) * E_ND * N;
-  size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * MT_BLOCKS * MT_N * N;
+  size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * (MT_BLOCKS * MT_N * (size_t)c.N + MT_PAD);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_mt);
   if (hipMalloc(&h->blob, total) != hipSuccess) {

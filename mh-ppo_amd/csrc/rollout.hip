@@ -230,17 +230,10 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   // One pedestrian and a compile-time S that is a multiple of 4: this env's selected
   // feature rows are feat_c[e][0..S)[0] = S*13 contiguous floats on both sides, 16-B
   // aligned (S*52 B per env), copied as float4s.
-  constexpr bool feat_rows_contiguous = EV::CNS > 0 && EV::CNS % 4 == 0 && EV::CNP == 1;
-  if constexpr (feat_rows_contiguous) {
-    constexpr int NV = EV::CNS * NF_C / 4;
-    const float4 *fs = reinterpret_cast<const float4 *>(B.feat_c + (size_t)e * (EV::CNS * NF_C));
-    float4 *fo = reinterpret_cast<float4 *>(B.obs_c + ((size_t)t * c.N + e) * (EV::CNS * NF_C));
-    float4 v[NV];
-#pragma unroll
-    for (int k = 0; k < NV; k++) v[k] = fs[k];
-#pragma unroll
-    for (int k = 0; k < NV; k++) fo[k] = v[k];
-  }
+  // With one pedestrian the selected feature row of every slot is THE row, so obs_c[t] is
+  // feat_c verbatim: the host points feat_c at obs_c[t] for the policy step (rollout.py
+  // collect) and nothing is copied here.  Otherwise each slot's selected row is copied.
+  const bool feat_in_place = B.feat_c == B.obs_c + (size_t)t * c.N * S * NF_C && P == 1;
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t row0 = ((size_t)e * S + i) * P;
@@ -258,7 +251,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     const size_t bt = ((size_t)t * c.N + e) * S + i;  // time-major records [T][N][S]
     B.act[bt] = a;
     B.logp[bt] = mvn_logp(a, loc);
-    if (!feat_rows_contiguous) {
+    if (!feat_in_place) {
       const float *fs = B.feat_c + (row0 + sel) * NF_C;
       float *fo = B.obs_c + bt * NF_C;
 #pragma unroll
@@ -390,7 +383,7 @@ __global__ void __launch_bounds__(TPB) k_eval_step(Cfg c, Bufs eb, mhppo_mlp mc,
   E.trig[e] = trig;
   if (saved) {  // (:224-229)
     for (int i = 0; i < S; i++) E.rews_d[te * S + i] = (float)epm[i];
-    for (int p = 0; p < P; p++) E.waiting[te * P + p] = (float)eb.ped[((size_t)P_WT * P + p) * N + e];
+    for (int p = 0; p < P; p++) E.waiting[te * P + p] = (float)eb.ped[sidx(P_NF * P, P_WT * P + p, e)];
   }
 }
 

@@ -137,6 +137,8 @@ class RolloutGPU:
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
         for t in range(self.T):
+            if self.P == 1:  # features straight into the step's record (include/mhppo.h)
+                self._bufs.feat_c = self.obs_c[t].data_ptr()
             _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
                                               ctypes.byref(self._bufs), st))
             if step_events is not None:  # HIP events bracketing the env-step kernel on this stream

@@ -20,13 +20,13 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   HostEnv *h = new HostEnv();
   build_cfg(*cfg, h->c);
   const Cfg &c = h->c;
-  size_t N = c.N;
+  size_t N = npad(c.N);
   h->b.car = (double *)calloc((size_t)C_NF * c.nC * N, 8);
   h->b.ped = (double *)calloc((size_t)P_NF * c.P * N, 8);
   h->b.pfl = (uint32_t *)calloc((size_t)c.P * N, 4);
   h->b.envd = (double *)calloc((size_t)E_ND * N, 8);
   h->b.envi = (int32_t *)calloc((size_t)EI_NI * N, 4);
-  h->b.mt = (uint32_t *)calloc((size_t)MT_BLOCKS * MT_N * N, 4);
+  h->b.mt = (uint32_t *)calloc((size_t)MT_BLOCKS * MT_N * c.N + MT_PAD, 4);
   for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
   return h;
 }
