@@ -82,6 +82,13 @@ int mhppo_env_import(mhppo_env *env, const void *src, void *stream);
  * scalable :884-946).  obs: float32 [N, obs_dim] or NULL. */
 int mhppo_env_reset(mhppo_env *env, float *obs, void *stream);
 
+/* Replaces Env_rollout.choix_test (Coop-MH-PPO-scalable.py:629-633) + env.get_state(), the
+ * scripted scenario evaluate(n, choix=True) plays after every reset (:170-172): cross 3,
+ * pedestrians rebuilt with pedestrian 0 crossing from (0, -1) at 1.25 m/s, cars 0/1 at -45 /
+ * -22 m on lanes 0 / 1.  Scalable env only (MHPPO_EINVAL otherwise).  obs: float32
+ * [N, obs_dim] or NULL. */
+int mhppo_env_choix_test(mhppo_env *env, float *obs, void *stream);
+
 /* Replaces Crosswalk_*.step(actions) (Env_hybrid_multi_coop.py:745-832; 4cars :783-844;
  * scalable :789-878).  actions: float64 [N, 2S] = [acc_0..acc_{S-1}, light_0..light_{S-1}];
  * obs float32 [N, obs_dim] (nullable); rewards, reward_light float64 [N, S];

@@ -218,6 +218,67 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   E.save_rng();
 }
 
+// ------------------------------------------------------------ choix_test
+// Env_rollout.choix_test (Coop-MH-PPO-scalable.py:629-633) right after a reset, then the
+// driver's env.get_state() (:171-172); scalable env (oracle_env_choix_test restates it):
+// cross = 3; every pedestrian rebuilt non-crossing / non-existent (reset_pedestrian
+// :948-955, their draws), pedestrian 0 reset_ped (:106-134) to speed (0, 1.25) at (0, -1),
+// direction +1, ped_left = -1 and ped_in_cross = cross as VALUES (the observation shows
+// them; the flags hold their truthiness, which is all the dynamics read before the next
+// step's boolean_ped_position), a CG_score draw, the sin profile; cars 0/1 reset_car
+// (:583-587) to (state["car"][1], -45 / -22, light 0, lane 0 / 1), state["car"][1] being
+// car 0's float32 observed speed.  (NumPy >= 2 would then step cars 0/1 in float32 — NEP 50
+// on that np.float32 speed; the reference's pinned NumPy 1.26 promotes to float64, as here.)
+template <int V>
+MHPPO_HD void env_choix_test_one(const Cfg &c, const Bufs &b, int e, float *obs) {
+  Env<V> E(c, b, e);
+  const double v0 = (double)(float)(E.car(C_EXIST, 0) != 0.0 ? E.car(C_VC, 0) : 0.0);
+  E.cross = 3.0;
+  E.cl = (double)c.nb_lines * E.cross;
+  b.envd[sidx(E_ND, E_CROSS, e)] = E.cross;
+  for (int p = 0; p < c.P; p++) {
+    Ped q;
+    ped_init(E, q, 0, 0);
+    store_ped(E, p, q, false);
+  }
+  Ped q = load_ped(E, 0);
+  q.ivx = 0.0;
+  q.ivy = 1.25;
+  q.Vx = q.ivx;
+  q.Vy = q.ivy;
+  q.Sx = 0.0;
+  q.Sy = -1.0;
+  q.ratio = q.ivx / (q.ivy + 1e-3);
+  q.dir = 1;
+  q.lpos = (double)(c.nb_lines * (q.dir < 0) - 1 * (q.dir > 0));
+  q.delta = 0.0;
+  q.set(F_EXIST, true);
+  q.set(F_LEFT, true);     // leave = -1 (truthy)
+  q.set(F_INCROSS, true);  // CZ = cross = 3. (truthy)
+  q.set(F_ISCROSS, true);
+  (void)CG_score(E, q, E.cl);  // self.CG = CG_score(cross_lines): its normalvariate draw
+  q.set(F_SIN, c.sin_model != 0);
+  q.A = q.B = q.W = 0.0;
+  if (c.sin_model) {
+    const double abs_speed = fabs(q.ivy);
+    const double T = E.cl / (abs_speed + 10e-3);
+    const int check = ((abs_speed * PI) / 2.0 <= 2.5);
+    q.A = (double)check * PI * abs_speed / 2.0 + (double)(!check) * (2.5 - abs_speed) / (1.0 - (2.0 / PI));
+    q.B = (double)(!check) * (2.5 - q.A);
+    q.W = PI / T;
+  }
+  store_ped(E, 0, q, false);
+  E.car(C_SC, 0) = -45.0; E.car(C_VC, 0) = v0; E.car(C_LIGHT, 0) = 0.0; E.car(C_LINE, 0) = 0.0;
+  E.car(C_SC, 1) = -22.0; E.car(C_VC, 1) = v0; E.car(C_LIGHT, 1) = 0.0; E.car(C_LINE, 1) = 1.0;
+  env_observe(E, 0, obs);
+  if (obs) {  // get_data shows ped_left / ped_in_cross as stored: -1 and 3.0
+    float *o = obs + (size_t)e * c.obs_dim + (c.obs_dim - 9 * c.P);
+    o[5] = -1.0f;
+    o[6] = (float)E.cross;
+  }
+  E.save_rng();
+}
+
 // ------------------------------------------------------------------ step
 // act: this env's [2 nS] actions [acc..., light...]; rw/rl: this env's [nAV] outputs (nullable)
 // act: [2 nS] (pointer or array type); per-AV rewards land in E.rw / E.rl

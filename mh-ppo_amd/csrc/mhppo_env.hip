@@ -25,6 +25,12 @@ __global__ void __launch_bounds__(TPB) k_env_reset(Cfg c, Bufs b, float *obs) {
   if (e < c.N) env_reset_one<V>(c, b, e, obs);
 }
 
+__global__ void __launch_bounds__(TPB) k_env_choix(Cfg c, Bufs b, float *obs) {
+  int e = blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(b, c.N, e, e < c.N);
+  if (e < c.N) env_choix_test_one<V_SCALABLE>(c, b, e, obs);
+}
+
 template <int V>
 __global__ void __launch_bounds__(TPB)
     k_env_step(Cfg c, Bufs b, const double *actions, float *obs, double *rew, double *rlight, uint8_t *done) {
@@ -176,6 +182,18 @@ int mhppo_env_reset(mhppo_env *env, float *obs, void *stream) {
   if (!env) return set_error(MHPPO_EINVAL, "null env");
   dim3 grid((env->c.N + TPB - 1) / TPB);
   VARIANT_LAUNCH(k_env_reset, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, obs);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_env_choix_test(mhppo_env *env, float *obs, void *stream) {
+  if (!env) return set_error(MHPPO_EINVAL, "null env");
+  if (env->c.variant != V_SCALABLE || env->c.nS < 2)
+    return set_error(MHPPO_EINVAL, "choix_test is the scalable driver's scenario (Coop-MH-PPO-scalable.py:629-633); "
+                                   "the coop/naif drivers' version calls reset_pedestrian with 8 of its 10 "
+                                   "arguments and raises TypeError");
+  dim3 grid((env->c.N + TPB - 1) / TPB);
+  hipLaunchKernelGGL(k_env_choix, grid, dim3(TPB), 0, (hipStream_t)stream, env->c, env->b, obs);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

@@ -53,6 +53,7 @@ _SIGS = {
     "mhppo_env_reward_slots": (I32, [P]),
     "mhppo_env_state_dim": (I32, [P]),
     "mhppo_env_reset": (I32, [P, P, P]),
+    "mhppo_env_choix_test": (I32, [P, P, P]),
     "mhppo_env_state_bytes": (I64, [P]),
     "mhppo_env_export": (I32, [P, P, P]),
     "mhppo_env_import": (I32, [P, P, P]),

@@ -62,11 +62,10 @@ class Env_rollout:
 
     def iterations(self, actor_net_cross, actor_net_wait, actor_net_choice, nbr_episodes, choix=False):
         """Deterministic evaluation (:152-252) of `nbr_episodes` consecutive episodes in every
-        env; returns (obs, acts, rews_c, rews_d, waiting_time) env-major (see RolloutGPU.evaluate)."""
-        if choix:
-            raise NotImplementedError("choix_test scripted scenario (:629-633) is not part of this build")
+        env; returns (obs, acts, rews_c, rews_d, waiting_time) env-major (see RolloutGPU.evaluate).
+        choix=True: the scripted choix_test scenario (:629-633) after every reset."""
         with torch.no_grad():
-            return self.gpu.evaluate(actor_net_cross, actor_net_wait, actor_net_choice, nbr_episodes)
+            return self.gpu.evaluate(actor_net_cross, actor_net_wait, actor_net_choice, nbr_episodes, choix=choix)
 
     def iterations_rand(self, actor_net_cross, actor_net_wait, actor_net_choice, cov_mat=None, cov_mat_d=None,
                         batch_size=None, random_rate=0.0, forced_choice=None, eps_tape=None):

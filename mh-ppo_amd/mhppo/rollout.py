@@ -70,12 +70,13 @@ class RolloutGPU:
         b.T = self.T
         self._bufs = b
 
-    def evaluate(self, actor_cross, actor_wait, actor_choice, episodes=1):
+    def evaluate(self, actor_cross, actor_wait, actor_choice, episodes=1, choix=False):
         """Deterministic evaluation (Env_rollout.iterations :152-252): `episodes` consecutive
         episodes in every env (env e's episodes continue its own random stream).
         Returns the five tensors iterations returns, env-major (env 0's episodes first),
         on the env's device: obs [N*K*T, obs_dim], acts [N*K*T, S], rews_c [N*K*T, S]
-        (float32), rews_d [saves, S], waiting [saves * P]."""
+        (float32), rews_d [saves, S], waiting [saves * P].  choix=True plays the scripted
+        choix_test scenario (:629-633) after every reset (scalable env only)."""
         L = _lib.lib()
         venv, N, S, P, T = self.venv, self.N, self.S, self.P, self.T
         dev = venv.device
@@ -96,6 +97,8 @@ class RolloutGPU:
                 setattr(b, k, ctypes.c_void_p(v.data_ptr()))
             b.T = T
             _lib.check(L.mhppo_env_reset(venv.handle, _lib.ptr(E["obs"]), st))
+            if choix:  # iterations(choix=True): choix_test + get_state (:170-172)
+                _lib.check(L.mhppo_env_choix_test(venv.handle, _lib.ptr(E["obs"]), st))
             for t in range(T):
                 _lib.check(L.mhppo_eval_step(venv.handle, ctypes.byref(mc), ctypes.byref(mw), ctypes.byref(md), t,
                                              ctypes.byref(b), st))

@@ -45,6 +45,8 @@ def lib():
         L.oracle_env_step.argtypes = [P, P, P, P, P]
         L.oracle_env_dump.restype = I
         L.oracle_env_dump.argtypes = [P, P]
+        L.oracle_env_choix_test.restype = I
+        L.oracle_env_choix_test.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -83,6 +85,13 @@ class OracleEnv:
     def reset(self):
         o = np.zeros(self.obs_dim, np.float32)
         lib().oracle_env_reset(self.h, _p(o))
+        return o
+
+    def choix_test(self):
+        """Env_rollout.choix_test (:629-633) + get_state: the scripted scenario's observation."""
+        o = np.zeros(self.obs_dim, np.float32)
+        if lib().oracle_env_choix_test(self.h, _p(o)) != 0:
+            raise ValueError("choix_test is defined for the scalable env only")
         return o
 
     def step(self, actions):
@@ -161,7 +170,7 @@ def rollout(variant, nb_car, nb_ped, nb_lines, seeds, w_cross, w_wait, w_choice,
 
 
 def evaluate(variant, nb_car, nb_ped, nb_lines, seeds, episodes, w_cross, w_wait, w_choice, mean=-1.0, std=3.0,
-             acc_lo=-4.0, acc_hi=2.0, dt=0.3, T=80):
+             acc_lo=-4.0, acc_hi=2.0, dt=0.3, T=80, choix=False):
     """Algo_PPO.evaluate (:738-747) restated: Env_rollout.reset() — which resets the env,
     consuming that reset's draws (:125-129) — then Env_rollout.iterations (deterministic
     evaluation): for each seed, `episodes` consecutive episodes on one env.  Returns a list (one per seed) of dicts shaped like
@@ -172,7 +181,7 @@ def evaluate(variant, nb_car, nb_ped, nb_lines, seeds, episodes, w_cross, w_wait
     L.oracle_eval_episode.restype = ctypes.c_int
     L.oracle_eval_episode.argtypes = [P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_, P_,
                                       ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,
-                                      ctypes.c_double] + [P_] * 6
+                                      ctypes.c_double] + [P_] * 6 + [ctypes.c_int]
     S = 2 * nb_lines if variant == "scalable" else nb_car
     wc, ww, wd = (np.ascontiguousarray(w, np.float32) for w in (w_cross, w_wait, w_choice))
     res = []
@@ -187,7 +196,10 @@ def evaluate(variant, nb_car, nb_ped, nb_lines, seeds, episodes, w_cross, w_wait
                      rews_d=np.zeros((T, S), np.float32), waiting=np.zeros((T, nb_ped), np.float32))
             n = L.oracle_eval_episode(env.h, VARIANTS[variant], S, nb_ped, T, _p(wc), _p(ww), _p(wd), mean, std,
                                       acc_lo, acc_hi, dt, *[_p(o[k]) for k in ("obs", "acts", "rews_c", "saved",
-                                                                             "rews_d", "waiting")])
+                                                                             "rews_d", "waiting")],
+                                      int(bool(choix)))
+            if n < 0:
+                raise ValueError("choix_test is defined for the scalable env only (:629-633)")
             sv = o["saved"][:n].astype(bool)
             acc["obs"].append(o["obs"][:n])
             acc["acts"].append(o["acts"][:n])

@@ -716,6 +716,57 @@ void oracle_env_reset(OEnv *e, float *obs) {
     e->episode_length = (double)(e->max_episode - 1) * e->dt;
 }
 
+/* Env_rollout.choix_test (Coop-MH-PPO-scalable.py:629-633) on the scalable env, then the
+ * driver's env.get_state() (:171-172):
+ *   env.cross = 3.
+ *   env.reset_pedestrian(0, 0., 1.25, 0., -1.0, 0, -1, env.cross, True, 1)
+ *     (Env_hybrid_multi_coop_scalable.py:948-955: every pedestrian rebuilt non-crossing and
+ *     non-existent — their draws — then pedestrian 0's reset_ped :106-134: speeds, position,
+ *     ratio, direction +1, line_pos, delta 0, exist, ped_left = -1, ped_in_cross = cross
+ *     (values, not booleans, until the next step's boolean_ped_position), is_crossing, a
+ *     CG_score(cross_lines) draw, the sin profile)
+ *   env.reset_cars(0, state["car"][1], -45, 0., 0.); env.reset_cars(1, state["car"][1], -22, 0., 1.)
+ *     (:957-958, car.reset_car :583-587; state["car"][1] = car 0's float32 observed speed)
+ *   get_state (:960-968): every car slot visible.
+ * Returns -1 for the other variants (their drivers' choix_test raise TypeError). */
+int oracle_env_choix_test(OEnv *e, float *obs) {
+    if (e->variant != V_SCALABLE || e->nS < 2) return -1;
+    const double v0 = (double)(float)(e->cars[0].exist ? e->cars[0].Vc : 0.0);
+    e->cross = 3.;
+    for (int i = 0; i < e->nb_ped; i++) ped_init(e, &e->peds[i], 0, 0);
+    Ped *p = &e->peds[0];
+    p->init_speed[0] = 0.; p->init_speed[1] = 1.25;
+    p->init_pos[0] = 0.; p->init_pos[1] = -1.0;
+    p->Vp_x = p->init_speed[0]; p->Vp_y = p->init_speed[1];
+    p->Sp_x = p->init_pos[0]; p->Sp_y = p->init_pos[1];
+    p->ratio = p->init_speed[0] / (p->init_speed[1] + 1e-3);
+    p->direction = 1;
+    p->line_pos = (double)(p->max_lines * (p->direction < 0) - 1 * (p->direction > 0));
+    p->delta = 0;
+    p->exist = 1;
+    p->ped_left = -1;
+    p->ped_in_cross = 3; /* CZ = env.cross = 3. */
+    p->is_crossing = 1;
+    p->CG = ped_CG_score(e, p, p->cross_lines);
+    p->sin_model = e->sin_model;
+    if (p->sin_model) {
+        p->t_init = 0.0;
+        double abs_speed = fabs(p->init_speed[1]);
+        p->T = p->cross_lines / (abs_speed + 10e-3);
+        int check = ((abs_speed * PI) / 2.0 <= p->Vm);
+        p->A = (double)check * PI * abs_speed / 2.0 + (double)(!check) * (p->Vm - abs_speed) / (1.0 - (2.0 / PI));
+        p->B = (double)(!check) * (p->Vm - p->A);
+        p->w = PI / p->T;
+    }
+    e->cars[0].Sc = -45.; e->cars[0].Vc = v0; e->cars[0].light = 0.; e->cars[0].line = 0.;
+    e->cars[1].Sc = -22.; e->cars[1].Vc = v0; e->cars[1].light = 0.; e->cars[1].line = 1.;
+    CarView cv;
+    cv.n = 0;
+    for (int i = 0; i < e->nS; i++) view_add(&cv, &e->cars[i]);
+    write_obs(e, &cv, obs);
+    return 0;
+}
+
 int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards, double *reward_light) {
     const int v = e->variant;
     const int nS = e->nS;

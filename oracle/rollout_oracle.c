@@ -30,6 +30,7 @@ int oracle_env_obs_dim(const OEnv *e);
 void oracle_env_reset(OEnv *e, float *obs);
 int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards, double *reward_light);
 int oracle_env_dump(const OEnv *e, double *out);
+int oracle_env_choix_test(OEnv *e, float *obs);
 
 #define NF 13
 
@@ -267,13 +268,14 @@ int oracle_rollout_episode(OEnv *e, int variant, int S, int P, int T, const floa
 int oracle_eval_episode(OEnv *e, int variant, int S, int P, int T, const float *w_cross, const float *w_wait,
                         const float *w_choice, float act_mean, float act_std, double acc_lo, double acc_hi,
                         double dt, float *o_obs, float *o_acts, float *o_rews_c, uint8_t *o_saved, float *o_rews_d,
-                        float *o_waiting) {
+                        float *o_waiting, int choix) {
     Lay L = layout(variant, S, P);
     const int dc = oracle_choice_dim(variant, S), od = oracle_env_obs_dim(e);
     float obs[1024];
     double actions[64], rew[32], rl[32], epr[32], dump[4096];
     int a_d[256];
     oracle_env_reset(e, obs);
+    if (choix && oracle_env_choix_test(e, obs) != 0) return -1;  /* iterations(choix=True) :170-172 */
     int need = 1, t;
     for (t = 0; t < T; t++) {
         if (need) {

@@ -29,6 +29,14 @@ CASES = {  # name: (driver, variant, nb_car, nb_ped, nb_lines, envs, episodes, s
     "scalable_211": ("scalable", "scalable", 2, 1, 1, 4, 2, 920, "pappo-scalable-coop-{h}-111-{k}-step-1000.pth"),
     # nb_ped 2: envs drawing ped_traffic = 1 < nb_ped re-decide every step (:218-220)
     "scalable_221": ("scalable", "scalable", 2, 2, 1, 4, 2, 930, "pappo-scalable-coop-{h}-111-{k}-step-1000.pth"),
+    # evaluate(n, choix=True): Env_rollout.choix_test (:629-633) after every reset (:170-172)
+    "scalable_choix_211": ("scalable", "scalable", 2, 1, 1, 4, 2, 940, "pappo-scalable-coop-{h}-111-{k}-step-1000.pth",
+                           True),
+    "scalable_choix_221": ("scalable", "scalable", 2, 2, 1, 4, 2, 950, "pappo-scalable-coop-{h}-111-{k}-step-1000.pth",
+                           True),
+    # two lanes (choix_test puts car 1 on lane 1): no shipped weights of that width, so the
+    # heads are torch.manual_seed(960) random inits (packed into the fixture like the others)
+    "scalable_choix_422": ("scalable", "scalable", 4, 2, 2, 4, 2, 960, None, True),
 }
 
 
@@ -37,17 +45,18 @@ def packed(net):
                       for p in (lay.weight, lay.bias)]).numpy()
 
 
-def run(driver, variant, nc, npd, nl, E, K, seed_base, wfmt):
+def run(driver, variant, nc, npd, nl, E, K, seed_base, wfmt, choix=False):
     env = R.make(variant, nc, npd, nl)
     S = 2 * nl if variant == "scalable" else nc
     glob = dict(env=env, nb_lines=nl, nb_car=nc, nb_ped=npd)
     ns = refclasses.scalable_classes(**glob) if driver == "scalable" else refclasses.notebook_classes(driver, **glob)
     Model_PPO, Env_rollout = ns["Model_PPO"], ns["Env_rollout"]
     dc = 2 + 6 * (S - 1) + 10 if driver == "scalable" else 2 + 5 * (S - 1) + 10
+    torch.manual_seed(seed_base)
     ac = Model_PPO(13, 1, 1, nb_car=S, mean=-1.0, std=3.0)
     aw = Model_PPO(13, 1, 1, nb_car=S, mean=-1.0, std=3.0)
     ad = Model_PPO(dc, 2, 2)
-    for net, h in ((ac, "cross"), (aw, "wait"), (ad, "choice")):
+    for net, h in ((ac, "cross"), (aw, "wait"), (ad, "choice")) if wfmt else ():
         sd = torch.load(os.path.join(WDIR, wfmt.format(h=h, k="actor")), weights_only=True, map_location="cpu")
         net.load_state_dict(sd)
     with contextlib.redirect_stdout(open(os.devnull, "w")):
@@ -57,19 +66,21 @@ def run(driver, variant, nc, npd, nl, E, K, seed_base, wfmt):
         st = R.Stream(seed_base + e)
         with st.active():
             ro.reset()
-            obs, acts, rc, rd, wt = ro.iterations(ac, aw, ad, K)
+            obs, acts, rc, rd, wt = ro.iterations(ac, aw, ad, K, choix=choix)
         recs.append(dict(obs=obs.numpy(), acts=acts.numpy().reshape(len(obs), -1), rews_c=rc.numpy(),
                          rews_d=rd.numpy().reshape(-1, S), waiting=wt.numpy().reshape(-1)))
     out = dict(driver=driver, variant=variant, nb_car=nc, nb_ped=npd, nb_lines=nl, seed_base=seed_base,
-               episodes=K, w_cross=packed(ac), w_wait=packed(aw), w_choice=packed(ad))
+               episodes=K, choix=bool(choix), w_cross=packed(ac), w_wait=packed(aw), w_choice=packed(ad))
     for k in recs[0]:
         out[k] = np.concatenate([r[k] for r in recs])
         out["n_" + k] = np.array([len(r[k]) for r in recs])
     return out
 
 
-def main():
+def main(only=None):
     for name, case in CASES.items():
+        if only and name not in only:
+            continue
         d = run(*case)
         path = os.path.join(OUT, f"eval_{name}.npz")
         np.savez_compressed(path, **d)
@@ -78,4 +89,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -44,3 +44,24 @@ def test_device_source_matches_reference(hostsim, path, view):
         assert np.array_equal(rl, g["reward_light"][:, t]), t
         assert np.array_equal(d, g["done"][:, t]), t
         assert np.array_equal(h.state()[:, :k], g["dump"][:, t]), t
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 1), (4, 2, 2), (8, 1, 4)])
+def test_device_choix_test_matches_oracle(hostsim, shape):
+    """choix_test (:629-633) + get_state, then 80 steps: the device source on the CPU
+    equals the C oracle bit for bit (observations, rewards, reward_light)."""
+    import oracle
+    nc, npd, nl = shape
+    N = 6
+    h = hostsim.HostVec("scalable", N, nc, npd, nl, seed_base=515)
+    orc = [oracle.OracleEnv("scalable", nc, npd, nl, seed=515 + e) for e in range(N)]
+    assert np.array_equal(h.reset(), np.stack([o.reset() for o in orc]))
+    assert np.array_equal(h.choix_test(), np.stack([o.choix_test() for o in orc]))
+    S = 2 * nl
+    rng = np.random.default_rng(1)
+    for t in range(80):
+        a = np.concatenate([rng.uniform(-4, 2, (N, S)), np.where(rng.random((N, S)) < 0.5, -1.0, 1.0)], 1)
+        hs = h.step(a)
+        os_ = [o.step(a[e]) for e, o in enumerate(orc)]
+        for j in range(3):
+            assert np.array_equal(hs[j], np.stack([x[j] for x in os_])), (t, j)

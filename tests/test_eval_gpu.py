@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_oracle_eval import CASES, check_eval
+from test_oracle_eval import CASES, CHOIX_CASES, TOL_CHOIX, check_eval
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
@@ -23,10 +23,10 @@ def _nets(wc, ww, wd, dc):
     return ac, aw, ad
 
 
-def _evaluate(venv, nets, K):
+def _evaluate(venv, nets, K, choix=False):
     from mhppo.rollout import RolloutGPU
     venv.reset(want_obs=False)  # Env_rollout.reset() before iterations (:744, :129)
-    out = RolloutGPU(venv).evaluate(*nets, K)
+    out = RolloutGPU(venv).evaluate(*nets, K, choix=choix)
     return dict(zip(KEYS, (t.cpu().numpy() for t in out)))
 
 
@@ -69,3 +69,42 @@ def test_algo_evaluate_api():
     assert obs.shape == (8 * 3 * 80, venv.obs_dim) and acts.shape == (8 * 3 * 80, 2) and rc.shape == acts.shape
     assert rd.shape == (8 * 3, 2) and wt.shape == (8 * 3,)
     assert torch.isfinite(obs).all() and torch.isfinite(acts).all()
+
+
+@pytest.mark.parametrize("name", CHOIX_CASES)
+def test_gpu_eval_choix_matches_reference(name):
+    """evaluate(n, choix=True): the scripted choix_test scenario after every reset."""
+    import oracle
+    from mhppo.env import VecCrosswalk
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"eval_{name}.npz"))
+    E, K, variant = len(g["n_obs"]), int(g["episodes"]), str(g["variant"])
+    venv = VecCrosswalk(variant, E, int(g["nb_car"]), int(g["nb_ped"]), int(g["nb_lines"]),
+                        seed_base=int(g["seed_base"]))
+    nets = _nets(g["w_cross"], g["w_wait"], g["w_choice"], oracle.choice_dim(variant, venv.n_slots))
+    out = _evaluate(venv, nets, K, choix=True)
+    assert np.array_equal(out["obs"][0], g["obs"][0])  # the scripted observation
+    check_eval(out, g, tol=TOL_CHOIX)
+
+
+def test_gpu_eval_choix_matches_oracle_many_envs():
+    import oracle
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    torch.manual_seed(8)
+    venv = VecCrosswalk("scalable", 64, 4, 2, 2, seed_base=5151)
+    dc = oracle.choice_dim("scalable", venv.n_slots)
+    w = [Model_PPO(13, 1, 1).packed().numpy(), Model_PPO(13, 1, 1).packed().numpy(),
+         Model_PPO(dc, 2, 2).packed().numpy()]
+    out = _evaluate(venv, _nets(*w, dc), 2, choix=True)
+    res = oracle.evaluate("scalable", 4, 2, 2, [5151 + e for e in range(64)], 2, *w, choix=True)
+    check_eval(out, {k: np.concatenate([r[k] for r in res]) for k in res[0]})
+
+
+def test_choix_rejected_off_scalable():
+    from mhppo.algo import Algo_PPO
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    algo = Algo_PPO(Model_PPO, VecCrosswalk("coop", 4, 2, 1, 2, seed_base=1), verbose=False)
+    from mhppo._lib import MhppoError
+    with pytest.raises(MhppoError):
+        algo.evaluate(1, choix=True)

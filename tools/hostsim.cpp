@@ -45,6 +45,11 @@ int hs_reward_slots(HostEnv *h) { return h->c.nAV; }
 void hs_reset(HostEnv *h, float *obs) {
   for (int e = 0; e < h->c.N; e++) HS_DISPATCH(env_reset_one<V>(h->c, h->b, e, obs));
 }
+int hs_choix(HostEnv *h, float *obs) {
+  if (h->c.variant != V_SCALABLE) return -1;
+  for (int e = 0; e < h->c.N; e++) env_choix_test_one<V_SCALABLE>(h->c, h->b, e, obs);
+  return 0;
+}
 void hs_step(HostEnv *h, const double *a0, float *obs, double *rew0, double *rl0, uint8_t *done) {
   const int S = h->c.nS, R = h->c.nAV;
   for (int e = 0; e < h->c.N; e++) {

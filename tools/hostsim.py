@@ -18,6 +18,7 @@ for n in ("hs_obs_dim", "hs_state_dim"):
     getattr(L, n).restype = ctypes.c_int
     getattr(L, n).argtypes = [P]
 L.hs_reset.argtypes = [P, P]
+L.hs_choix.argtypes = [P, P]
 L.hs_step.argtypes = [P, P, P, P, P, P]
 L.hs_state.argtypes = [P, P]
 
@@ -48,6 +49,11 @@ class HostVec:
     def reset(self):
         o = np.zeros((self.N, self.obs_dim), np.float32)
         L.hs_reset(self.h, _p(o))
+        return o
+
+    def choix_test(self):
+        o = np.zeros((self.N, self.obs_dim), np.float32)
+        assert L.hs_choix(self.h, _p(o)) == 0
         return o
 
     def step(self, a):
