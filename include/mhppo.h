@@ -137,8 +137,11 @@ typedef struct mhppo_rollout_bufs {
     double *rew, *ep_min;
     uint8_t *exist;
     int32_t *rows;
-    int32_t T, reserved;
+    int32_t T, flags;   /* flags: MHPPO_ROLLOUT_* */
 } mhppo_rollout_bufs;
+/* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
+ * instead of the MFMA kernel; both are bit-identical (A/B and tests) */
+#define MHPPO_ROLLOUT_VALU_POLICY 1
 
 int mhppo_choice_dim(const mhppo_env *env);
 

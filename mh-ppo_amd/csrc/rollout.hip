@@ -12,6 +12,8 @@
 // Update-time kernels (advantage stats/normalise, PPO surrogates, MSE) are
 // elementwise + deterministic two-pass reductions (fixed summation order).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <string.h>
 
@@ -157,7 +159,135 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
   B.out_c[r] = t + (head ? mean_w : mean_c);
 }
 
-// Head lists for k_policy_sorted (stable: each list in row order).  Pass 1 counts the
+// ------------------------------------------------------- MFMA policy step
+// k_policy_mfma: the head-sorted rows as 32-row tiles on f32 MFMA (v_mfma_f32_32x32x2_f32, the
+// forward layout of mlp_train.hip: rows on the lanes, features in the 16 C registers), both
+// actors' weights in LDS.  Bit-identical to mlp_forward13_rows: the f32 MFMA is a k-ordered
+// fmaf chain (cdna_hip_programming.md §3), and the weight rows of layers 1-3 are staged
+// permuted so that C register s of lane half kh holds neuron 2s + kh — k-step s of the next
+// layer then feeds its inputs 2s, 2s + 1, i.e. every chain runs in ascending input order;
+// the 32 -> 1 output is the same ascending fmaf chain over both lane halves.
+namespace pol {
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int S1 = 15, S2 = 33, S3 = 65;  // odd LDS row strides: conflict-free operand reads
+constexpr int O_W1 = 0, O_B1 = O_W1 + 32 * S1, O_W2 = O_B1 + 32, O_B2 = O_W2 + 64 * S2, O_W3 = O_B2 + 64,
+              O_B3 = O_W3 + 32 * S3, O_W4 = O_B3 + 32, O_B4 = O_W4 + 32, HEAD = (O_B4 + 1 + 3) / 4 * 4;
+// C-tile row i = (r & 3) + 8 (r >> 2) + 4 kh of register r carries neuron 2 r + kh
+__device__ __forceinline__ int neuron_of_row(int i) { return 2 * ((i & 3) + 4 * (i >> 3)) + ((i >> 2) & 1); }
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; i++) z[i] = 0.0f;
+  return z;
+}
+// v[r] = relu(v[r] + b[row(r)]) with the oracle's relu (x < 0 ? 0 : x)
+__device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
+  const float4 *b4 = reinterpret_cast<const float4 *>(b);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const float4 c = b4[2 * q + kh];
+    v[4 * q + 0] = relu(v[4 * q + 0] + c.x);
+    v[4 * q + 1] = relu(v[4 * q + 1] + c.y);
+    v[4 * q + 2] = relu(v[4 * q + 2] + c.z);
+    v[4 * q + 3] = relu(v[4 * q + 3] + c.w);
+  }
+}
+// one 13 -> 32 -> 64 -> 32 -> 1 actor (torch-packed W) into LDS, rows permuted as above
+__device__ void stage(float *L, const float *__restrict__ W, int tid, int nt) {
+  const float *w1 = W, *b1 = w1 + 32 * NF_C, *w2 = b1 + 32, *b2 = w2 + 2048, *w3 = b2 + 64, *b3 = w3 + 2048,
+              *w4 = b3 + 32, *b4 = w4 + 32;
+  for (int x = tid; x < 32 * S1; x += nt) {
+    const int i = x / S1, k = x % S1;
+    L[O_W1 + x] = k < NF_C ? w1[neuron_of_row(i) * NF_C + k] : 0.0f;
+  }
+  for (int x = tid; x < 32; x += nt) {
+    L[O_B1 + x] = b1[neuron_of_row(x)];
+    L[O_B3 + x] = b3[neuron_of_row(x)];
+    L[O_W4 + x] = w4[x];
+  }
+  for (int x = tid; x < 64 * 32; x += nt) {
+    const int i = x >> 5, k = x & 31;
+    L[O_W2 + i * S2 + k] = w2[((i & 32) + neuron_of_row(i & 31)) * 32 + k];
+  }
+  for (int x = tid; x < 64; x += nt) L[O_B2 + x] = b2[(x & 32) + neuron_of_row(x & 31)];
+  for (int x = tid; x < 32 * 64; x += nt) {
+    const int i = x >> 6, k = x & 63;
+    L[O_W3 + i * S3 + k] = w3[neuron_of_row(i) * 64 + k];
+  }
+  if (tid == 0) L[O_B4] = b4[0];
+}
+}  // namespace pol
+
+template <int V>
+__global__ void __launch_bounds__(TPB) k_policy_mfma(Cfg c, const float *__restrict__ Wc,
+                                                     const float *__restrict__ Ww, float mean_c, float std_c,
+                                                     float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
+  using namespace pol;
+  extern __shared__ float lds[];  // [2][HEAD]: cross, wait
+  const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5;
+  const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (tid >> 6)));
+  const int nwaves = gridDim.x * (TPB / 64);
+  if ((int64_t)gw * 64 < c.N) mt_refill_wave<TPB / 64>(eb, c.N, gw * 64 + l, gw * 64 + l < c.N);
+  stage(lds, Wc, tid, TPB);
+  stage(lds + HEAD, Ww, tid, TPB);
+  __syncthreads();
+  const int R = c.N * c.nS * c.P;
+  const int32_t *__restrict__ rows = B.rows;
+  const int nc = __builtin_amdgcn_readfirstlane(rows[R]), nw = __builtin_amdgcn_readfirstlane(rows[R + 1]);
+  const int tc = (nc + 31) / 32, ntiles = tc + (nw + 31) / 32;
+  const ObsLayout L = obs_layout(c);
+  for (int tile = gw; tile < ntiles; tile += nwaves) {
+    const int head = tile >= tc;
+    const int k0 = head ? nc + 32 * (tile - tc) : 32 * tile, kend = head ? nc + nw : nc;
+    const float *Wl = lds + head * HEAD;
+    const bool valid = k0 + j < kend;
+    const int r = valid ? rows[k0 + j] : 0;
+    const int p = r % c.P, i = (r / c.P) % c.nS, e = r / (c.P * c.nS);
+    float f[NF_C + 1];
+    const float ex = obs_car_ped(B.obs + (size_t)e * L.obs_dim, L, i, p, f);
+    f[NF_C] = 0.0f;
+    if (valid && kh == 0) {
+      float *fo = B.feat_c + (size_t)r * NF_C;
+#pragma unroll
+      for (int q = 0; q < NF_C; q++) fo[q] = f[q];
+    }
+    f32x16 h1 = zero16();
+#pragma unroll
+    for (int s = 0; s < 7; s++) h1 = mfma(Wl[O_W1 + j * S1 + 2 * s + kh], kh ? f[2 * s + 1] : f[2 * s], h1);
+    bias_relu(h1, Wl + O_B1, kh);
+    f32x16 h2a = zero16(), h2b = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+      h2a = mfma(Wl[O_W2 + j * S2 + 2 * s + kh], h1[s], h2a);
+      h2b = mfma(Wl[O_W2 + (32 + j) * S2 + 2 * s + kh], h1[s], h2b);
+    }
+    bias_relu(h2a, Wl + O_B2, kh);
+    bias_relu(h2b, Wl + O_B2 + 32, kh);
+    f32x16 h3 = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 2 * s + kh], h2a[s], h3);
+#pragma unroll
+    for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 32 + 2 * s + kh], h2b[s], h3);
+    bias_relu(h3, Wl + O_B3, kh);
+    float y = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+      const float own = h3[s], oth = __shfl_xor(own, 32);
+      y = fmaf(Wl[O_W4 + 2 * s], kh ? oth : own, y);
+      y = fmaf(Wl[O_W4 + 2 * s + 1], kh ? own : oth, y);
+    }
+    const float out = y + Wl[O_B4];
+    if (valid && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)
+      const float t = tanhf(out) * (head ? std_w : std_c);  // Model_PPO type 1 (:87-89)
+      B.out_c[r] = t + (head ? mean_w : mean_c);
+    }
+  }
+}
+
+// Head lists for k_policy_sorted / k_policy_mfma (stable: each list in row order).  Pass 1 counts the
 // cross rows of each 256-row block; pass 2 has every block sum the counts before it
 // (and all of them, for the wait list's base), then place its rows by wave prefix.
 __global__ void __launch_bounds__(TPB) k_head_count(const int32_t *a_d, int R, int32_t *cnt) {
@@ -666,6 +796,25 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
   const Cfg &c = env_cfg(env);
   size_t R = (size_t)c.N * c.nS * c.P;
   if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
+  if (bufs->rows && !(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
+    // persistent 32-row MFMA tiles: 2 blocks per CU, and at least N/64 waves (MT refill)
+    static int cus[16] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!cus[dev & 15]) {
+      int n = 256;
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      cus[dev & 15] = n;
+    }
+    const size_t tiles = R / 32 + 2, waves_env = ((size_t)c.N + 63) / 64;
+    size_t blocks = std::min<size_t>((size_t)2 * cus[dev & 15], (tiles + 3) / 4);
+    blocks = std::max<size_t>(blocks, (waves_env + 3) / 4);
+    VLAUNCH(k_policy_mfma, c.variant, dim3((unsigned)blocks), 2 * pol::HEAD * sizeof(float), (hipStream_t)stream, c,
+            actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std, actor_wait->mean,
+            actor_wait->std, *bufs, env_bufs(env));
+    CHECK_HIP(hipGetLastError());
+    return MHPPO_OK;
+  }
   if (bufs->rows) {
     // one wave per 64 rows of one head: at most R/64 + 2 waves, and at least N/64 (MT refill)
     const size_t waves = (R + 63) / 64 + 2;

@@ -33,7 +33,7 @@ class RolloutBatch:
 
 
 class RolloutGPU:
-    def __init__(self, venv, T=None):
+    def __init__(self, venv, T=None, valu_policy=False):
         if venv.variant == "4cars2":
             raise ValueError("4cars2 is an env-level variant only: the reference has no driver for it and its "
                              "PPO-driven followers earn no reward (Env_hybrid_multi_coop_4cars2.py:836-847)")
@@ -68,6 +68,8 @@ class RolloutGPU:
                      "logp", "rew", "ep_min", "exist", "rows"):
             setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
         b.T = self.T
+        # policy step on the VALU kernel instead of the MFMA one (bit-identical; A/B and tests)
+        b.flags = 1 if valu_policy else 0  # MHPPO_ROLLOUT_VALU_POLICY
         self._bufs = b
 
     def evaluate(self, actor_cross, actor_wait, actor_choice, episodes=1, choix=False):

@@ -105,3 +105,24 @@ def test_rollout_is_shard_invariant():
         parts.append(_gpu_out(ro.collect(ac, aw, ad, seed=1, iteration=2)))
     for k in a:
         assert np.array_equal(a[k], np.concatenate([parts[0][k], parts[1][k]])), k
+
+
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 2, 4), ("stop", 2, 2, 2)])
+def test_mfma_policy_bit_identical_to_valu(case):
+    """The MFMA policy kernel (k_policy_mfma: permuted weight rows so every f32-MFMA fmaf
+    chain runs in ascending input order) and the VALU one (k_policy_sorted) give the same
+    episode bit for bit, ragged last tiles included (N*S*P not a multiple of 32)."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    v, nc, npd, nl = case
+    outs = []
+    for valu in (False, True):
+        ro = RolloutGPU(VecCrosswalk(v, 300, nc, npd, nl, seed_base=777), valu_policy=valu)
+        torch.manual_seed(5)
+        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        ad = Model_PPO(ro.dc, 2, 2).cuda()
+        outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=2, iteration=1)))
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
