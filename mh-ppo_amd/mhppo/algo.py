@@ -133,7 +133,9 @@ class Algo_PPO:
             for net in self.nets():  # replicas start identical (rank 0's init)
                 for p in net.parameters():
                     dist.broadcast(p.data, src=0)
-        A = torch.optim.Adam
+        # one fused Adam launch per net and step on the GPU (the reference's default Adam
+        # semantics: lr, betas (0.9, 0.999), eps 1e-8, no weight decay)
+        A = (lambda params, lr: torch.optim.Adam(params, lr, fused=True)) if dev.type == "cuda" else torch.optim.Adam
         self.optimizer_critic_cross = A(self.critic_net_cross.parameters(), self.critic_lr)
         self.optimizer_critic_wait = A(self.critic_net_wait.parameters(), self.critic_lr)
         self.optimizer_critic_choice = A(self.critic_net_choice.parameters(), self.critic_d_lr)

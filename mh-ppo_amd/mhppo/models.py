@@ -37,6 +37,58 @@ class Model_PPO(nn.Module):
             self.layer4 = nn.Linear(32, nb_outputs)
             self.return_layer = nn.Tanh()
         torch.nn.init.orthogonal_(self.layer4.weight)
+        self._flatten()
+
+    # ---- flat storage: the parameters (and their .grad) are views of ONE contiguous
+    # float32 vector in the packed torch layout W1 b1 W2 b2 W3 b3 W4 b4, so the HIP kernels
+    # read the weights and write the gradient in place (no per-launch cat / copy), and one
+    # fused Adam launch updates a whole net.
+    def _params(self):
+        return [p for lay in (self.layer1, self.layer2, self.layer3, self.layer4) for p in (lay.weight, lay.bias)]
+
+    def _flatten(self):
+        ps = self._params()
+        flat = torch.cat([p.detach().reshape(-1) for p in ps]).float().contiguous()
+        gflat = torch.zeros_like(flat)
+        off = 0
+        with torch.no_grad():
+            for p in ps:
+                n = p.numel()
+                p.data = flat[off:off + n].view_as(p)
+                p.grad = gflat[off:off + n].view_as(p)
+                off += n
+        self._flat, self._gflat = flat, gflat
+
+    def _apply(self, fn, *args, **kwargs):
+        super()._apply(fn, *args, **kwargs)  # .to()/.cuda() move each parameter: re-flatten
+        self._flatten()
+        return self
+
+    def flat(self):
+        """The live flat parameter vector (no copy); re-flattens if a parameter was rebound."""
+        off = 0
+        base = self._flat.data_ptr()
+        for p in self._params():
+            if p.data_ptr() != base + 4 * off or p.dtype != torch.float32:
+                self._flatten()
+                return self._flat
+            off += p.numel()
+        return self._flat
+
+    def grad_flat(self):
+        """The flat gradient vector the parameters' .grad views alias (re-linked if
+        zero_grad(set_to_none=True) or autograd replaced a .grad)."""
+        self.flat()
+        off = 0
+        base = self._gflat.data_ptr()
+        for p in self._params():
+            n = p.numel()
+            if p.grad is None or p.grad.data_ptr() != base + 4 * off:
+                if p.grad is not None:
+                    self._gflat[off:off + n].copy_(p.grad.reshape(-1))
+                p.grad = self._gflat[off:off + n].view_as(p)
+            off += n
+        return self._gflat
 
     def forward(self, input1):
         if isinstance(input1, np.ndarray):
@@ -82,8 +134,8 @@ class Model_PPO(nn.Module):
         return self
 
     def mlp_desc(self, packed=None):
-        """(mhppo_mlp struct, backing tensor) for the C-ABI."""
-        t = self.packed() if packed is None else packed
+        """(mhppo_mlp struct, backing tensor) for the C-ABI (the live flat weights)."""
+        t = self.flat() if packed is None else packed
         d = _lib.Mlp()
         d.packed = ctypes.c_void_p(t.data_ptr())
         d.n_in, d.n_out = self.n_in, self.n_out

@@ -33,6 +33,22 @@ def _allreduce_(t):
     return t
 
 
+def _allreduce_net_grads(*nets):
+    """One all-reduce (SUM) of the nets' flat gradients (the .grad views alias them)."""
+    if not _dp():
+        return
+    if all(hasattr(n, "grad_flat") for n in nets):
+        flats = [n.grad_flat() for n in nets]
+        flat = torch.cat(flats)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        off = 0
+        for f in flats:
+            f.copy_(flat[off:off + f.numel()])
+            off += f.numel()
+        return
+    _allreduce_grads([p for n in nets for p in n.parameters()])
+
+
 def _allreduce_grads(params):
     if not _dp():
         return
@@ -141,9 +157,13 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     V = torch.empty(M, dtype=torch.float32, device=dev) if kind == KIND_CRITIC else value.detach().float().contiguous()
     act = None if act is None else act.float().contiguous()
     logp_old = None if logp_old is None else logp_old.float().contiguous()
-    grad = torch.empty(n_params(net.n_in, net.n_out), dtype=torch.float32, device=dev)
+    np_ = n_params(net.n_in, net.n_out)
+    # the gradient lands straight in the net's flat .grad storage when it has one
+    grad = net.grad_flat() if hasattr(net, "grad_flat") else None
+    if grad is None or grad.numel() != np_ or grad.device != dev:
+        grad = torch.empty(np_, dtype=torch.float32, device=dev)
     sums = torch.zeros(3, dtype=torch.float64, device=dev)
-    w = net.packed()
+    w = net.flat() if hasattr(net, "flat") else net.packed()
     p = _lib.ptr
     ev = None
     if TRAIN_EVENTS is not None:
@@ -166,6 +186,8 @@ def normalized_advantage(ret, value, m_global):
 
 
 def _set_grads(net, flat):
+    if hasattr(net, "_gflat") and flat is net._gflat:
+        return  # written in place (k_mlp_train)
     off = 0
     for lay in (net.layer1, net.layer2, net.layer3, net.layer4):
         for p in (lay.weight, lay.bias):
@@ -188,7 +210,7 @@ def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
     ga, sa, _ = k_mlp_train(KIND_CONT, actor, obs, ret, V, act, logp_old, stats, m_global=m_global)
     _set_grads(critic, gc)
     _set_grads(actor, ga)
-    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+    _allreduce_net_grads(actor, critic)
     opt_actor.step()
     opt_critic.step()
     return sa[0:1], sc[0:1]
@@ -227,7 +249,7 @@ def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
                                 m_global=m_global)
         _set_grads(critic, gc)
         _set_grads(actor, ga)
-        _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+        _allreduce_net_grads(actor, critic)
         opt_actor.step()
         opt_critic.step()
         return sa[0:1], sc[0:1]
@@ -240,7 +262,7 @@ def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
                             m_global=m_global)
     _set_grads(critic, gc)
     _set_grads(actor, ga)
-    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
+    _allreduce_net_grads(actor, critic)
     opt_actor.step()
     opt_critic.step()
     return sa[0:1], sc[0:1]
