@@ -34,29 +34,49 @@
 namespace mhppo {
 
 // Phase timing, A/B builds only (tools/ab_build.sh <name> -DMHPPO_TIMING): lane 0 of every
-// wave adds the shader-clock cycles since its previous mark to g_timing[k] (mark 0 starts
-// the clock, g_timing[15] counts waves); tools/env_phases.py reads them.  Loads are
+// wave adds the shader-clock cycles since its previous mark to its phase-k slot (mark 0
+// starts the clock); MHPPO_MARK_FLUSH adds the wave's slots to g_timing[k] and counts the
+// wave in g_timing[15]; tools/env_phases.py / train_phases.py read them.  Loads are
 // asynchronous, so a phase is charged with the wait for the data it first consumes.
 #if defined(MHPPO_TIMING) && defined(__HIP_DEVICE_COMPILE__)
 static __device__ unsigned long long g_timing[16];
+// per-wave accumulators in LDS (one global atomic per phase and wave, at MHPPO_MARK_FLUSH)
+__device__ __forceinline__ unsigned long long *timing_slots() {
+  // [wave][phase 1..10 at 1..10, last stamp at 11]: 1.5 KB, within the train kernel's LDS slack
+  __shared__ unsigned long long t_acc[16][12];
+  return &t_acc[threadIdx.x >> 6][0];
+}
 __device__ __forceinline__ void timing_mark(int k) {
-  __shared__ unsigned long long t_last[16];
-  const int w = threadIdx.x >> 6;
+  unsigned long long *a = timing_slots();
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long now = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_sched_barrier(0);
   if ((threadIdx.x & 63) == 0) {
-    if (k > 0) atomicAdd(&g_timing[k], now - t_last[w]);
-    else atomicAdd(&g_timing[15], 1ull);
-    t_last[w] = now;
+    if (k > 0) {
+      a[k] += now - a[11];
+    } else {
+      for (int q = 0; q < 11; q++) a[q] = 0;
+    }
+    a[11] = now;
+  }
+}
+__device__ __forceinline__ void timing_flush() {
+  unsigned long long *a = timing_slots();
+  if ((threadIdx.x & 63) == 0) {
+    for (int q = 1; q < 11; q++)
+      if (a[q]) atomicAdd(&g_timing[q], a[q]);
+    atomicAdd(&g_timing[15], 1ull);
   }
 }
 #define MHPPO_MARK(k) ::mhppo::timing_mark(k)
+#define MHPPO_MARK_FLUSH() ::mhppo::timing_flush()
 #elif defined(MHPPO_TIMING) && defined(__HIP__)
 static __device__ unsigned long long g_timing[16];
 #define MHPPO_MARK(k)
+#define MHPPO_MARK_FLUSH()
 #else
 #define MHPPO_MARK(k)
+#define MHPPO_MARK_FLUSH()
 #endif
 
 enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP = 5 };
@@ -279,6 +299,7 @@ struct Env {
   static constexpr int VAR = V;
   static constexpr int MAXAV = 16;
   static constexpr int CNS = 0, CNP = 0;  // compile-time action slots / pedestrians: not known
+  static constexpr int OBS_DIM = 0;       // compile-time observation width: not known
   using AvArr = PlainArr<double, MAXAV>;
   AvArr rw, rl;  // step outputs per AV: reward, reward_light
   const Cfg &c;
@@ -322,6 +343,7 @@ struct EnvR {
   static constexpr int VAR = V;
   static constexpr int MAXAV = NAV;
   static constexpr int CNS = V == V_4CARS2 ? 2 * NAV : NAV, CNP = NP;
+  static constexpr int OBS_DIM = (V == V_SCALABLE ? 7 * NC + 4 : 6 * NC + 3) + 9 * NP;
   using AvArr = PlainArr<double, NAV>;
   AvArr rw, rl;  // step outputs per AV: reward, reward_light
   const Cfg &c;

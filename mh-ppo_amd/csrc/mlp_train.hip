@@ -280,6 +280,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
 
   int cb = 0;
+  MHPPO_MARK(0);
   if (PF && gw < nfull) prefetch_tile<KIND, LY>(ws + LY::O_IN, X, ret, V, act, lp_old, gw * 32, l);
   for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= (PF ? 1 : 0)) {
     const int64_t row0 = tile * 32;
@@ -299,6 +300,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
       load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
     }
     wave_sync();
+    MHPPO_MARK(1);  // tile inputs landed
     const float *Xs = slot + LY::IN_X;
     // ---- forward
     f32x16 h1 = zero16();
@@ -340,6 +342,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
       float part1 = dot16(lds + LY::O_W4 + 32, h3, kh);
       y1 = (part1 + __shfl_xor(part1, 32)) + b41;
     }
+    MHPPO_MARK(2);  // forward
     // ---- loss gradient dL/dy for this lane's row
     const bool valid = j < nrows;
     float dy0 = 0.0f, dy1 = 0.0f;
@@ -408,6 +411,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
         dy1 = (float)((double)p[1] * (g1 - dot));
       }
     }
+    MHPPO_MARK(3);  // loss gradient
     gB40 += (kh == 0) ? dy0 : 0.0f;
     gB41 += (kh == 0) ? dy1 : 0.0f;
     // ---- layer 4 backward: dW4 = rowsum(dy * h3), dH3 = W4^T dy masked
@@ -476,6 +480,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
       d2a[r] = ((m2 >> r) & 1u) ? d2a[r] : 0.0f;
       d2b[r] = ((m2 >> (16 + r)) & 1u) ? d2b[r] : 0.0f;
     }
+    MHPPO_MARK(4);  // layer-4 backward, dW3 + dH2
     wave_sync();
     phase();
     put_tile(T0, d2a, l);
@@ -500,6 +505,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     for (int s = 0; s < 16; s++) d1 = mfma(lds[LY::O_W2 + (32 + feat(s, l)) * S2 + j], d2b[s], d1);
 #pragma unroll
     for (int r = 0; r < 16; r++) d1[r] = (h1[r] > 0.0f) ? d1[r] : 0.0f;
+    MHPPO_MARK(5);  // dW2 + dH1
     wave_sync();
     phase();
     put_tile(T0, d1, l);
@@ -515,7 +521,9 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     }
     wave_sync();
     phase();
+    MHPPO_MARK(6);  // dW1 (timing builds only)
   }
+  MHPPO_MARK_FLUSH();
   // ---- write this wave's partial gradient (packed torch layout)
   float *gp = gpart + (size_t)gw * NWP;
 #pragma unroll
@@ -609,6 +617,17 @@ void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int n
                      packed, X, nin, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, gp, dp);
 }
 }  // namespace
+
+#ifdef MHPPO_TIMING
+// A/B timing builds only (not in include/mhppo.h): copy out and clear this TU's g_timing
+extern "C" int mhppo_debug_timing_train(unsigned long long *out16) {
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)));
+  return MHPPO_OK;
+}
+#endif
 
 extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const float *X, int64_t M, const float *ret,
                                float *value, const float *act, const float *logp_old, const double *stats,

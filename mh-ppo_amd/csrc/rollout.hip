@@ -364,6 +364,9 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   // feat_c verbatim: the host points feat_c at obs_c[t] for the policy step (rollout.py
   // collect) and nothing is copied here.  Otherwise each slot's selected row is copied.
   const bool feat_in_place = B.feat_c == B.obs_c + (size_t)t * c.N * S * NF_C && P == 1;
+  // compile-time S multiple of 4: the step's act/logp/rew/ep_min records go out as vectors
+  constexpr bool REC_VEC = EV::CNS > 0 && EV::CNS % 4 == 0;
+  float av[REC_VEC ? EV::CNS : 1], lv[REC_VEC ? EV::CNS : 1];
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t row0 = ((size_t)e * S + i) * P;
@@ -379,8 +382,13 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     float z = eps[(size_t)e * S + i];
     float a = loc + MVN_L * z;
     const size_t bt = ((size_t)t * c.N + e) * S + i;  // time-major records [T][N][S]
-    B.act[bt] = a;
-    B.logp[bt] = mvn_logp(a, loc);
+    if constexpr (REC_VEC) {
+      av[i] = a;
+      lv[i] = mvn_logp(a, loc);
+    } else {
+      B.act[bt] = a;
+      B.logp[bt] = mvn_logp(a, loc);
+    }
     if (!feat_in_place) {
       const float *fs = B.feat_c + (row0 + sel) * NF_C;
       float *fo = B.obs_c + bt * NF_C;
@@ -391,18 +399,43 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     int cp = B.closest[(size_t)e * S + i];
     act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
   }
+  if constexpr (REC_VEC) {  // this env's S records of step t are contiguous and 16-B aligned
+    const size_t b0 = ((size_t)t * c.N + e) * S;
+#pragma unroll
+    for (int q = 0; q < EV::CNS / 4; q++) {
+      reinterpret_cast<float4 *>(B.act + b0)[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+      reinterpret_cast<float4 *>(B.logp + b0)[q] = make_float4(lv[4 * q], lv[4 * q + 1], lv[4 * q + 2], lv[4 * q + 3]);
+    }
+  }
+  // the episodic minima are read with the other inputs, not behind the env step's stores
+  // (which the compiler may not reorder them across): no memory round trip at the end
+  PlainArr<double, EV::MAXAV> epm;
+  MHPPO_UNROLL
+  for (int i = 0; i < S; i++) epm[i] = B.ep_min[(size_t)e * S + i];
   MHPPO_MARK(3);
   env_step_body(E, act, B.obs, nullptr);
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
-    const size_t bt = ((size_t)t * c.N + e) * S + i;
-    B.rew[bt] = E.rw[i];
-    double m = B.ep_min[(size_t)e * S + i];
+    double m = epm[i];
     double x = E.rl[i];
-    // np.minimum: NaN-propagating
-    B.ep_min[(size_t)e * S + i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));
+    epm[i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));  // np.minimum: NaN-propagating
+  }
+  if constexpr (REC_VEC) {
+    const size_t b0 = ((size_t)t * c.N + e) * S;
+#pragma unroll
+    for (int q = 0; q < EV::CNS / 2; q++) {
+      reinterpret_cast<double2 *>(B.rew + b0)[q] = make_double2(E.rw[2 * q], E.rw[2 * q + 1]);
+      reinterpret_cast<double2 *>(B.ep_min + (size_t)e * S)[q] = make_double2(epm[2 * q], epm[2 * q + 1]);
+    }
+  } else {
+    MHPPO_UNROLL
+    for (int i = 0; i < S; i++) {
+      B.rew[((size_t)t * c.N + e) * S + i] = E.rw[i];
+      B.ep_min[(size_t)e * S + i] = epm[i];
+    }
   }
   MHPPO_MARK(10);
+  MHPPO_MARK_FLUSH();
 }
 
 template <int V>
@@ -420,7 +453,7 @@ __global__ void __launch_bounds__(TPB)
 template <int V, int NC, int NAV, int NP, bool REFILL>
 __global__ void __launch_bounds__(TPB)
     k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
-  int e = blockIdx.x * TPB + threadIdx.x;
+  const int e = blockIdx.x * TPB + threadIdx.x;
   MHPPO_MARK(0);
   if (REFILL) mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
   MHPPO_MARK(1);
@@ -737,10 +770,11 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
     return false;
   } else {
     if (!use_reg_view(c, V, NC, NAV, NP)) return false;
+    const dim3 g = grid_for(c.N);
     if (B.rows)
-      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
     else
-      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), grid_for(c.N), dim3(TPB), 0, s, c, eb, eps, t, B);
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
     return true;
   }
 }

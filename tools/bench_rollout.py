@@ -1,0 +1,28 @@
+"""Rollout collect timing (80 steps of policy + env kernels, 65536 4cars envs), HIP events per kernel."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
+from mhppo.algo import Algo_PPO  # noqa: E402
+from mhppo.env import VecCrosswalk  # noqa: E402
+from mhppo.models import Model_PPO  # noqa: E402
+
+venv = VecCrosswalk("4cars", 65536, 4, 1, 2, seed_base=0)
+torch.manual_seed(0)
+algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
+T = 80
+with torch.no_grad():
+    for it in range(3):
+        ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(T)]
+        algo.rollout.reset()
+        a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
+                                 iteration=it, step_events=ev)
+        b.record()
+        torch.cuda.synchronize()
+        env_us = sum(e0.elapsed_time(e1) for e0, e1 in ev) / T * 1e3
+        print(f"iter {it}: collect {a.elapsed_time(b):.2f} ms, env kernel {env_us:.1f} us/step", flush=True)
