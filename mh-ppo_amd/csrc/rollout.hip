@@ -167,6 +167,9 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
 // permuted so that C register s of lane half kh holds neuron 2s + kh — k-step s of the next
 // layer then feeds its inputs 2s, 2s + 1, i.e. every chain runs in ascending input order;
 // the 32 -> 1 output is the same ascending fmaf chain over both lane halves.
+#ifndef MHPPO_POLICY_BLOCKS_PER_CU
+#define MHPPO_POLICY_BLOCKS_PER_CU 2  // persistent k_policy_mfma blocks per CU (A/B builds override)
+#endif
 namespace pol {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int S1 = 15, S2 = 33, S3 = 65;  // odd LDS row strides: conflict-free operand reads
@@ -239,16 +242,38 @@ __global__ void __launch_bounds__(TPB) k_policy_mfma(Cfg c, const float *__restr
   const int nc = __builtin_amdgcn_readfirstlane(rows[R]), nw = __builtin_amdgcn_readfirstlane(rows[R + 1]);
   const int tc = (nc + 31) / 32, ntiles = tc + (nw + 31) / 32;
   const ObsLayout L = obs_layout(c);
+  // software pipeline over this wave's tiles: row indices two tiles ahead, the rows'
+  // observation values one tile ahead, so the gathers overlap the MFMA work
+  auto tile_row = [&](int tl, bool &ok) {
+    const int hd = tl >= tc;
+    const int a0 = hd ? nc + 32 * (tl - tc) : 32 * tl, a1 = hd ? nc + nw : nc;
+    ok = tl < ntiles && a0 + j < a1;
+    return ok ? rows[a0 + j] : 0;
+  };
+  auto raw_of = [&](int rr) {
+    const int pp = rr % c.P, ii = (rr / c.P) % c.nS, ee = rr / (c.P * c.nS);
+    return feat_raw(B.obs + (size_t)ee * L.obs_dim, L, ii, pp);
+  };
+  bool ok_cur, ok_nxt;
+  int r_cur = tile_row(gw, ok_cur);
+  int r_nxt = tile_row(gw + nwaves, ok_nxt);
+  FeatRaw raw_cur = raw_of(r_cur);
   for (int tile = gw; tile < ntiles; tile += nwaves) {
+    bool ok_2;
+    const int r_2 = tile_row(tile + 2 * nwaves, ok_2);
+    const FeatRaw raw_nxt = raw_of(r_nxt);
     const int head = tile >= tc;
-    const int k0 = head ? nc + 32 * (tile - tc) : 32 * tile, kend = head ? nc + nw : nc;
     const float *Wl = lds + head * HEAD;
-    const bool valid = k0 + j < kend;
-    const int r = valid ? rows[k0 + j] : 0;
-    const int p = r % c.P, i = (r / c.P) % c.nS, e = r / (c.P * c.nS);
+    const bool valid = ok_cur;
+    const int r = r_cur;
     float f[NF_C + 1];
-    const float ex = obs_car_ped(B.obs + (size_t)e * L.obs_dim, L, i, p, f);
+    const float ex = obs_car_ped_raw(raw_cur, f);
     f[NF_C] = 0.0f;
+    r_cur = r_nxt;
+    ok_cur = ok_nxt;
+    r_nxt = r_2;
+    ok_nxt = ok_2;
+    raw_cur = raw_nxt;
     if (valid && kh == 0) {
       float *fo = B.feat_c + (size_t)r * NF_C;
 #pragma unroll
@@ -841,7 +866,7 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
       cus[dev & 15] = n;
     }
     const size_t tiles = R / 32 + 2, waves_env = ((size_t)c.N + 63) / 64;
-    size_t blocks = std::min<size_t>((size_t)2 * cus[dev & 15], (tiles + 3) / 4);
+    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev & 15], (tiles + 3) / 4);
     blocks = std::max<size_t>(blocks, (waves_env + 3) / 4);
     VLAUNCH(k_policy_mfma, c.variant, dim3((unsigned)blocks), 2 * pol::HEAD * sizeof(float), (hipStream_t)stream, c,
             actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std, actor_wait->mean,

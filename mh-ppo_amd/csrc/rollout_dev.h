@@ -70,12 +70,35 @@ MHPPO_HD inline void leave_cross(float car_line, float ped_pos, float ped_dir, f
   }
 }
 
+// The 13 observation values obs_car_ped reads for (car i, ped p), gathered apart from the
+// arithmetic so a kernel can issue the loads of the next row ahead of time.
+struct FeatRaw {
+  float car[6], ped[9], cl, lines;  // car[0,4] and ped[5,6] unused
+};
+MHPPO_HD inline FeatRaw feat_raw(const float *o, const ObsLayout &L, int i, int p) {
+  const float *car = o + i * L.cw;
+  const float *ped = o + L.ped_off + p * 9;
+  const float *env = o + L.env_off;
+  FeatRaw R;
+  R.car[0] = 0.f; R.car[1] = car[1]; R.car[2] = car[2]; R.car[3] = car[3]; R.car[4] = 0.f; R.car[5] = car[5];
+  R.ped[0] = ped[0]; R.ped[1] = ped[1]; R.ped[2] = ped[2]; R.ped[3] = ped[3]; R.ped[4] = ped[4];
+  R.ped[5] = 0.f; R.ped[6] = 0.f; R.ped[7] = ped[7]; R.ped[8] = ped[8];
+  R.cl = env[0];
+  R.lines = env[L.lines_idx];
+  return R;
+}
+MHPPO_HD inline float obs_car_ped_from(const float *car, const float *ped, float cl, float lines, float *f);
+
 // Env_rollout.obs_car_ped (:541-572): 13 features of (car i, ped p); returns ped exist
 MHPPO_HD inline float obs_car_ped(const float *o, const ObsLayout &L, int i, int p, float *f) {
   const float *car = o + i * L.cw;
   const float *ped = o + L.ped_off + p * 9;
   const float *env = o + L.env_off;
-  float cl = env[0], lines = env[L.lines_idx];
+  return obs_car_ped_from(car, ped, env[0], env[L.lines_idx], f);
+}
+MHPPO_HD inline float obs_car_ped_raw(const FeatRaw &R, float *f) { return obs_car_ped_from(R.car, R.ped, R.cl, R.lines, f); }
+
+MHPPO_HD inline float obs_car_ped_from(const float *car, const float *ped, float cl, float lines, float *f) {
   float crossing, dist_start, end_cross, dist_end;
   is_in_cross(car[5], ped[3], ped[8], cl, lines, crossing, dist_start);
   leave_cross(car[5], ped[3], ped[8], cl, lines, end_cross, dist_end);
