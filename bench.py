@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--nb-lines", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=256)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
     return ap.parse_args()
 
 
@@ -108,9 +110,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; with fewer GPUs than ranks (a rehearsal) ranks share them round-robin
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.dist_backend)
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
