@@ -17,10 +17,11 @@ WORKER = os.path.join(ROOT, "tests", "dp_worker.py")
 def test_two_ranks_equal_one_process(tmp_path):
     one, two = str(tmp_path / "one.npy"), str(tmp_path / "two.npy")
     env = dict(os.environ, OMP_NUM_THREADS="4")
-    subprocess.run([sys.executable, WORKER, "--out", one], check=True, timeout=240, env=env)
+    # cwd: Algo_PPO.train writes its reward curves to ./load_model/parameters, as the reference
+    subprocess.run([sys.executable, WORKER, "--out", one], check=True, timeout=240, env=env, cwd=tmp_path)
     subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                     "--master-addr", "127.0.0.1", "--master-port", str(29600 + os.getpid() % 300), WORKER,
-                    "--out", two], check=True, timeout=240, env=env)
+                    "--out", two], check=True, timeout=240, env=env, cwd=tmp_path)
     a, b = np.load(one), np.load(two)
     assert a.shape == b.shape
     assert np.isfinite(a).all()
