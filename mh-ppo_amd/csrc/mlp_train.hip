@@ -234,6 +234,8 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
                 float *__restrict__ gpart, double *__restrict__ dpart) {
   constexpr int NOUT = KIND == K_CHOICE ? 2 : 1;
   using LY = Lay<KS, PF, NOUT>;
+  // 13-input heads: 13 < 2 KS = 14, so layer 1 has a free input column for the bias
+  constexpr bool FOLD_B1 = PF;
   constexpr int WAVES = LY::WAVES;
   extern __shared__ float lds[];
   const int tid = threadIdx.x, l = tid & 63;
@@ -245,7 +247,8 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   // ---- stage weights (padded strides, zero padding)
   for (int i = tid; i < 32 * LY::S1; i += 64 * WAVES) {
     const int r = i / LY::S1, c = i % LY::S1;
-    lds[LY::O_W1 + i] = c < nin ? W[G_W1 + r * nin + c] : 0.0f;
+    // FOLD_B1: b1 rides in the padding column nin of W1 against a constant-1 input
+    lds[LY::O_W1 + i] = c < nin ? W[G_W1 + r * nin + c] : ((FOLD_B1 && c == nin) ? W[G_B1 + r] : 0.0f);
   }
   for (int i = tid; i < 32; i += 64 * WAVES) lds[LY::O_B1 + i] = W[G_B1 + i];
   for (int i = tid; i < 64 * 32; i += 64 * WAVES) lds[LY::O_W2 + (i >> 5) * S2 + (i & 31)] = W[G_W2 + i];
@@ -308,10 +311,15 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     for (int s = 0; s < KS; s++) {
       int k = 2 * s + kh;
       float a = lds[LY::O_W1 + j * LY::S1 + k];
-      float b = (k < nin) ? Xs[j * nin + k] : 0.0f;
+      float b = (k < nin) ? Xs[j * nin + k] : ((FOLD_B1 && k == nin) ? 1.0f : 0.0f);
       h1 = mfma(a, b, h1);
     }
-    bias_relu(h1, lds + LY::O_B1, kh);
+    if constexpr (FOLD_B1) {  // the last fmaf of the chain added b1 (fma(b, 1, acc) == acc + b)
+#pragma unroll
+      for (int r = 0; r < 16; r++) h1[r] = relu0(h1[r]);
+    } else {
+      bias_relu(h1, lds + LY::O_B1, kh);
+    }
     phase();
     f32x16 h2a = zero16(), h2b = zero16();
 #pragma unroll
@@ -511,12 +519,12 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     put_tile(T0, d1, l);
     wave_sync();
     phase();
-    if (kh == 0) gB1 += row_sum(T0, l);
+    if (!FOLD_B1 && kh == 0) gB1 += row_sum(T0, l);  // FOLD_B1: column nin of dW1 is dB1
     // dW1 += dH1^T . X
 #pragma unroll
     for (int s = 0; s < 16; s++) {
       int k = 2 * s + kh;
-      float b = (j < nin) ? Xs[k * nin + j] : 0.0f;
+      float b = (j < nin) ? Xs[k * nin + j] : ((FOLD_B1 && j == nin) ? 1.0f : 0.0f);
       gW1 = mfma(T0[j * ST + k], b, gW1);
     }
     wave_sync();
@@ -530,13 +538,14 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   for (int r = 0; r < 16; r++) {
     int f = feat(r, l);
     if (j < nin) gp[G_W1 + f * nin + j] = gW1[r];
+    if (FOLD_B1 && j == nin) gp[G_B1 + f] = gW1[r];
     gp[G_W2 + f * 32 + j] = gW2a[r];
     gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
     gp[G_W3 + f * 64 + j] = gW3a[r];
     gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
   }
   if (kh == 0) {
-    gp[G_B1 + j] = gB1;
+    if (!FOLD_B1) gp[G_B1 + j] = gB1;
     gp[G_B3 + j] = gB3;
     gp[G_W4 + j] = gW40;
     if (NOUT == 2) gp[G_W4 + 32 + j] = gW41;
