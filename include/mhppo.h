@@ -191,6 +191,10 @@ int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_roll
 /* Philox-4x32-10 noise (perf mode): out[i] for counter (offset + i) under key `seed`. */
 int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
 int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
+/* rows x cols normals, out[r * cols + c] from counter (offset + r * stride + c): a rollout's
+ * per-step noise in one launch (the same values as `rows` calls of mhppo_philox_normal). */
+int mhppo_philox_normal_2d(uint64_t seed, uint64_t offset, uint64_t stride, float *out, int64_t rows,
+                           int64_t cols, void *stream);
 
 /* ---- returns / advantage / PPO losses (futur_rewards :658-684, train_model_c/_d :778-851) ---- */
 

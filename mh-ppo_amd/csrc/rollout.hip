@@ -596,6 +596,21 @@ __global__ void __launch_bounds__(TPB) k_philox(uint64_t seed, uint64_t off, flo
   }
 }
 
+// rows x cols standard normals, element (r, c) from counter off + r * stride + c (one
+// launch for a whole rollout's per-step MVN noise: bit-identical to `rows` 1-D calls)
+__global__ void __launch_bounds__(TPB) k_philox_normal_2d(uint64_t seed, uint64_t off, uint64_t stride, float *out,
+                                                          int64_t rows, int64_t cols) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols, cc = i - r * cols;
+  const uint64_t ctr = off + (uint64_t)r * stride + (uint64_t)cc;
+  uint32_t c4[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x6d687070u, 0u};
+  philox(c4, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u1 = ((float)(c4[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+  const float u2 = (float)(c4[1] >> 8) * (1.0f / 16777216.0f);
+  out[i] = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
+}
+
 // ------------------------------------------------------------ returns
 // futur_rewards (:668-672): episodic_reward = rew + 0.99*episodic_reward, float64,
 // then torch.tensor(..., dtype=float) -> float32
@@ -933,6 +948,16 @@ int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, v
   if (!out || n < 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (n == 0) return MHPPO_OK;
   hipLaunchKernelGGL(k_philox, grid_for(n), dim3(TPB), 0, (hipStream_t)stream, seed, offset, out, n, 1);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_philox_normal_2d(uint64_t seed, uint64_t offset, uint64_t stride, float *out, int64_t rows, int64_t cols,
+                           void *stream) {
+  if (!out || rows < 0 || cols < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  if (rows == 0 || cols == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_philox_normal_2d, grid_for((size_t)(rows * cols)), dim3(TPB), 0, (hipStream_t)stream, seed,
+                     offset, stride, out, rows, cols);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

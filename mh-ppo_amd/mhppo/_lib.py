@@ -70,6 +70,7 @@ _SIGS = {
                               ctypes.POINTER(EvalBufs), P]),
     "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
+    "mhppo_philox_normal_2d": (I32, [U64, U64, U64, P, I64, I64, P]),
     "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_returns_scan_tm": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_adv_stats": (I32, [P, P, I64, P, P]),

@@ -119,9 +119,9 @@ class RolloutGPU:
         off = int(self.venv.cfg.env_id_offset)
         st = _lib.stream_ptr()
         _lib.check(L.mhppo_philox_uniform(key, off * self.S * self.P, _lib.ptr(self.u), self.u.numel(), st))
-        for t in range(self.T):
-            _lib.check(L.mhppo_philox_normal(key, (t + 1) * _CTR_STEP + off * self.S, _lib.ptr(self.eps[t]),
-                                             self.eps[t].numel(), st))
+        # step t's normals from counters (t + 1) * 2^40 + global (env, slot): one launch
+        _lib.check(L.mhppo_philox_normal_2d(key, _CTR_STEP + off * self.S, _CTR_STEP, _lib.ptr(self.eps), self.T,
+                                            self.eps[0].numel(), st))
 
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
                 eps_tape=None, step_events=None):

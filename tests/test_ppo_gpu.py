@@ -156,3 +156,17 @@ def test_fused_choice_grads_vs_autograd(M, dc):
     gat = torch.cat([g.reshape(-1) for g in torch.autograd.grad(probs, list(actor.parameters()), dp)])
     assert abs(float(sa[0]) - float(la[0])) <= 1e-5 * abs(float(la[0])) + 1e-6
     _close_grad(ga, gat)
+
+
+def test_philox_normal_2d_equals_rows():
+    """The one-launch rollout noise (mhppo_philox_normal_2d) is bit-identical to one
+    mhppo_philox_normal call per step (the counters of rollout.py's draw_noise)."""
+    from mhppo import _lib
+    L = _lib.lib()
+    rows, cols, stride, off = 5, 1000, 1 << 40, (1 << 40) + 777
+    a = torch.empty((rows, cols), device="cuda")
+    _lib.check(L.mhppo_philox_normal_2d(12345, off, stride, _lib.ptr(a), rows, cols, _lib.stream_ptr()))
+    b = torch.empty((rows, cols), device="cuda")
+    for r in range(rows):
+        _lib.check(L.mhppo_philox_normal(12345, off + r * stride, _lib.ptr(b[r]), cols, _lib.stream_ptr()))
+    assert torch.equal(a, b)
