@@ -79,6 +79,10 @@ struct Lay {
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ int feat(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -266,6 +270,9 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 
   // persistent accumulators
   f32x16 gW1 = zero16(), gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
+  // 13-input heads: dW1 = dH1^T X is [32 features x 14 columns] — two 16x16 tiles of the
+  // 16x16x4 MFMA (half the cycles of one 32x32 tile); D row (l>>4)*4 + r, column l & 15
+  f32x4 gW1q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float gB1 = 0.f, gB2 = 0.f, gB3 = 0.f, gW40 = 0.f, gW41 = 0.f, gB40 = 0.f, gB41 = 0.f;
   // float64 running sums (loss, sum A, sum A^2) live in LDS, one slot per lane of the low
   // half-wave: keeping them in VGPRs spills, and a spill reload's vmcnt(0) drains the prefetch
@@ -521,11 +528,21 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     phase();
     if (!FOLD_B1 && kh == 0) gB1 += row_sum(T0, l);  // FOLD_B1: column nin of dW1 is dB1
     // dW1 += dH1^T . X
+    if constexpr (PF) {  // rows 4s..4s+3 per step, ascending: the same fmaf chain order
 #pragma unroll
-    for (int s = 0; s < 16; s++) {
-      int k = 2 * s + kh;
-      float b = (j < nin) ? Xs[k * nin + j] : ((FOLD_B1 && j == nin) ? 1.0f : 0.0f);
-      gW1 = mfma(T0[j * ST + k], b, gW1);
+      for (int s = 0; s < 8; s++) {
+        const int rr = 4 * s + (l >> 4), jj = l & 15;
+        const float b = (jj < nin) ? Xs[rr * nin + jj] : ((FOLD_B1 && jj == nin) ? 1.0f : 0.0f);
+#pragma unroll
+        for (int ft = 0; ft < 2; ft++) gW1q[ft] = mfma16(T0[(16 * ft + (l & 15)) * ST + rr], b, gW1q[ft]);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        int k = 2 * s + kh;
+        float b = (j < nin) ? Xs[k * nin + j] : ((FOLD_B1 && j == nin) ? 1.0f : 0.0f);
+        gW1 = mfma(T0[j * ST + k], b, gW1);
+      }
     }
     wave_sync();
     phase();
@@ -537,12 +554,21 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 #pragma unroll
   for (int r = 0; r < 16; r++) {
     int f = feat(r, l);
-    if (j < nin) gp[G_W1 + f * nin + j] = gW1[r];
-    if (FOLD_B1 && j == nin) gp[G_B1 + f] = gW1[r];
+    if (!PF && j < nin) gp[G_W1 + f * nin + j] = gW1[r];
     gp[G_W2 + f * 32 + j] = gW2a[r];
     gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
     gp[G_W3 + f * 64 + j] = gW3a[r];
     gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
+  }
+  if constexpr (PF) {
+#pragma unroll
+    for (int ft = 0; ft < 2; ft++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int f = 16 * ft + (l >> 4) * 4 + r, jj = l & 15;
+        if (jj < nin) gp[G_W1 + f * nin + jj] = gW1q[ft][r];
+        if (FOLD_B1 && jj == nin) gp[G_B1 + f] = gW1q[ft][r];
+      }
   }
   if (kh == 0) {
     if (!FOLD_B1) gp[G_B1 + j] = gB1;
