@@ -143,19 +143,28 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   h->b.envd = (double *)p; p += al(bytes_envd);
   h->b.envi = (int32_t *)p; p += al(bytes_envi);
   h->b.mt = (uint32_t *)p;
-  hipMemset(h->blob, 0, total);
-  dim3 grid((c.N + TPB - 1) / TPB);
-  hipLaunchKernelGGL(k_env_seed, grid, dim3(TPB), 0, (hipStream_t)0, c, h->b);
-  CHECK_HIP(hipGetLastError());
-  CHECK_HIP(hipDeviceSynchronize());
+  // any failure past the allocation releases the blob and the handle before reporting
+  hipError_t e = hipMemset(h->blob, 0, total);
+  if (e == hipSuccess) {
+    dim3 grid((c.N + TPB - 1) / TPB);
+    hipLaunchKernelGGL(k_env_seed, grid, dim3(TPB), 0, (hipStream_t)0, c, h->b);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    (void)hipFree(h->blob);
+    delete h;
+    return set_error(MHPPO_EHIP, "env seeding failed: %s", hipGetErrorString(e));
+  }
   *out = h;
   return MHPPO_OK;
 }
 
 void mhppo_env_destroy(mhppo_env *env) {
   if (!env) return;
-  hipSetDevice(env->device);
-  hipFree(env->blob);
+  // destroy has no error channel: a failing device switch or free is not reportable here
+  (void)hipSetDevice(env->device);
+  (void)hipFree(env->blob);
   delete env;
 }
 

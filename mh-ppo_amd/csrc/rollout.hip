@@ -772,8 +772,8 @@ Scratch g_scratch[16];
 
 double *scratch(size_t n) {
   int dev = 0;
-  hipGetDevice(&dev);
-  Scratch &s = g_scratch[dev & 15];
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev > 15) return nullptr;
+  Scratch &s = g_scratch[dev];
   if (s.n < n) {
     if (s.p) (void)hipFree(s.p);
     if (hipMalloc(&s.p, n * sizeof(double)) != hipSuccess) {
