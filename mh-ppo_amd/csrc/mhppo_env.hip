@@ -120,7 +120,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
     return set_error(MHPPO_EINVAL, "scalable: nb_car must be <= 2*nb_lines (random.sample)");
   if (cfg->variant == V_NAIF && nS > 16) return set_error(MHPPO_EINVAL, "naif: at most 16 cars");
   if (!(cfg->car_b[0] < 0.0)) return set_error(MHPPO_EINVAL, "car_b[0][0] must be negative");
-  CHECK_HIP(hipSetDevice(device));
+  GUARD_DEVICE(device);
   mhppo_env *h = new mhppo_env();
   build_cfg(*cfg, h->c);
   const Cfg &c = h->c;
@@ -162,8 +162,9 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
 
 void mhppo_env_destroy(mhppo_env *env) {
   if (!env) return;
-  // destroy has no error channel: a failing device switch or free is not reportable here
-  (void)hipSetDevice(env->device);
+  // destroy has no error channel: a failing device switch or free is not reportable here;
+  // the caller's current device is restored either way (it may run from a GC finalizer)
+  mhppo::DeviceGuard g(env->device);
   (void)hipFree(env->blob);
   delete env;
 }
@@ -177,18 +178,21 @@ int64_t mhppo_env_state_bytes(const mhppo_env *env) { return env ? (int64_t)env-
 
 int mhppo_env_export(const mhppo_env *env, void *dst, void *stream) {
   if (!env || !dst) return set_error(MHPPO_EINVAL, "null argument");
+  GUARD_DEVICE(env->device);
   CHECK_HIP(hipMemcpyAsync(dst, env->blob, env->blob_bytes, hipMemcpyDefault, (hipStream_t)stream));
   return MHPPO_OK;
 }
 
 int mhppo_env_import(mhppo_env *env, const void *src, void *stream) {
   if (!env || !src) return set_error(MHPPO_EINVAL, "null argument");
+  GUARD_DEVICE(env->device);
   CHECK_HIP(hipMemcpyAsync(env->blob, src, env->blob_bytes, hipMemcpyDefault, (hipStream_t)stream));
   return MHPPO_OK;
 }
 
 int mhppo_env_reset(mhppo_env *env, float *obs, void *stream) {
   if (!env) return set_error(MHPPO_EINVAL, "null env");
+  GUARD_DEVICE(env->device);
   dim3 grid((env->c.N + TPB - 1) / TPB);
   VARIANT_LAUNCH(k_env_reset, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, obs);
   CHECK_HIP(hipGetLastError());
@@ -201,6 +205,7 @@ int mhppo_env_choix_test(mhppo_env *env, float *obs, void *stream) {
     return set_error(MHPPO_EINVAL, "choix_test is the scalable driver's scenario (Coop-MH-PPO-scalable.py:629-633); "
                                    "the coop/naif drivers' version calls reset_pedestrian with 8 of its 10 "
                                    "arguments and raises TypeError");
+  GUARD_DEVICE(env->device);
   dim3 grid((env->c.N + TPB - 1) / TPB);
   hipLaunchKernelGGL(k_env_choix, grid, dim3(TPB), 0, (hipStream_t)stream, env->c, env->b, obs);
   CHECK_HIP(hipGetLastError());
@@ -210,6 +215,7 @@ int mhppo_env_choix_test(mhppo_env *env, float *obs, void *stream) {
 int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *rewards, double *reward_light,
                    uint8_t *done, void *stream) {
   if (!env || !actions) return set_error(MHPPO_EINVAL, "null env/actions");
+  GUARD_DEVICE(env->device);
   dim3 grid((env->c.N + TPB - 1) / TPB);
   const Cfg &c = env->c;
 #define STEP_REG(V_, NC_, NAV_, NP_)                                                                    \
@@ -229,6 +235,7 @@ int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *re
 
 int mhppo_env_get_state(mhppo_env *env, double *out, void *stream) {
   if (!env || !out) return set_error(MHPPO_EINVAL, "null env/out");
+  GUARD_DEVICE(env->device);
   dim3 grid((env->c.N + TPB - 1) / TPB);
   int dim = mhppo_env_state_dim(env);
   VARIANT_LAUNCH(k_env_state, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, out, dim);
@@ -238,6 +245,7 @@ int mhppo_env_get_state(mhppo_env *env, double *out, void *stream) {
 
 int mhppo_env_get_rng(mhppo_env *env, uint32_t *mt, int32_t *mti, void *stream) {
   if (!env || !mt || !mti) return set_error(MHPPO_EINVAL, "null argument");
+  GUARD_DEVICE(env->device);
   size_t n = (size_t)env->c.N * 624;
   dim3 grid((unsigned)((n + TPB - 1) / TPB));
   hipLaunchKernelGGL(k_env_rng, grid, dim3(TPB), 0, (hipStream_t)stream, env->c, env->b, mt, mti);
@@ -251,4 +259,5 @@ int mhppo_env_get_rng(mhppo_env *env, uint32_t *mt, int32_t *mti, void *stream) 
 namespace mhppo {
 const Cfg &env_cfg(const mhppo_env *env) { return env->c; }
 const Bufs &env_bufs(const mhppo_env *env) { return env->b; }
+int env_device(const mhppo_env *env) { return env->device; }
 }  // namespace mhppo

@@ -641,7 +641,7 @@ struct Work {  // per-device partial buffers (calls on one device must share one
   int nw = 0;
   int cus = 0;
 };
-Work g_work[16];
+Work g_work[mhppo::MAX_DEVICES];
 
 template <int KIND, int KS, bool PF>
 void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int nin, int64_t M, const float *ret,
@@ -668,9 +668,14 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
                                float *value, const float *act, const float *logp_old, const double *stats,
                                const double *counts, double m_global, float out_mean, float out_std, float *grad,
                                double *sums, void *stream) {
-  if (!packed || !X || !ret || !value || !grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 ||
-      n_in > 32)
+  if (!grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 || n_in > 32)
     return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= 32)");
+  hipStream_t s = (hipStream_t)stream;
+  if (M == 0) {  // an empty shard (data parallel): zero gradient, sums unchanged; X/ret/value may be NULL
+    CHECK_HIP(hipMemsetAsync(grad, 0, sizeof(float) * n_params(n_in, kind == K_CHOICE ? 2 : 1), s));
+    return MHPPO_OK;
+  }
+  if (!packed || !X || !ret || !value) return set_error(MHPPO_EINVAL, "null packed/X/ret/value");
   if (kind == K_CONT && (n_in != NIN_CONT || !act || !logp_old || !stats))
     return set_error(MHPPO_EINVAL, "continuous actor pass needs n_in 13 and act/logp_old/stats");
   if (kind == K_CHOICE && (!logp_old || !stats || (!counts && !act)))
@@ -678,10 +683,10 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   if (M > ((int64_t)1 << 40)) return set_error(MHPPO_EINVAL, "M too large");
   const bool pf = n_in == NIN_CONT && kind != K_CHOICE;
   if (pf && ((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
-  hipStream_t s = (hipStream_t)stream;
   int dev = 0;
-  (void)hipGetDevice(&dev);
-  Work &wk = g_work[dev & 15];
+  CHECK_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
+  Work &wk = g_work[dev];
   if (wk.cus == 0) {
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -27,6 +27,7 @@ using namespace mhppo;
 namespace mhppo {
 const Cfg &env_cfg(const mhppo_env *env);
 const Bufs &env_bufs(const mhppo_env *env);
+int env_device(const mhppo_env *env);
 }  // namespace mhppo
 
 namespace {
@@ -772,7 +773,7 @@ Scratch g_scratch[16];
 
 double *scratch(size_t n) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev > 15) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= mhppo::MAX_DEVICES) return nullptr;
   Scratch &s = g_scratch[dev];
   if (s.n < n) {
     if (s.p) (void)hipFree(s.p);
@@ -839,6 +840,7 @@ int mhppo_choice_dim(const mhppo_env *env) { return env ? choice_dim(env_cfg(env
 int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const float *u, const int32_t *forced_a,
                         mhppo_rollout_bufs *bufs, void *stream) {
   if (!env || !actor_choice || !bufs || (!u && !forced_a)) return set_error(MHPPO_EINVAL, "null argument");
+  GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
   if (actor_choice->n_in != choice_dim(c) || actor_choice->n_out != 2)
     return set_error(MHPPO_EINVAL, "choice actor must be %d -> 2 (got %d -> %d)", choice_dim(c), actor_choice->n_in,
@@ -867,21 +869,22 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
   if (!env || !actor_cross || !actor_wait || !bufs) return set_error(MHPPO_EINVAL, "null argument");
   if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
     return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
+  GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
   size_t R = (size_t)c.N * c.nS * c.P;
   if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
   if (bufs->rows && !(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
     // persistent 32-row MFMA tiles: 2 blocks per CU, and at least N/64 waves (MT refill)
-    static int cus[16] = {0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (!cus[dev & 15]) {
+    static int cus[mhppo::MAX_DEVICES] = {0};
+    const int dev = env_device(env);
+    if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
+    if (!cus[dev]) {
       int n = 256;
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      cus[dev & 15] = n;
+      cus[dev] = n;
     }
     const size_t tiles = R / 32 + 2, waves_env = ((size_t)c.N + 63) / 64;
-    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev & 15], (tiles + 3) / 4);
+    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + 3) / 4);
     blocks = std::max<size_t>(blocks, (waves_env + 3) / 4);
     VLAUNCH(k_policy_mfma, c.variant, dim3((unsigned)blocks), 2 * pol::HEAD * sizeof(float), (hipStream_t)stream, c,
             actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std, actor_wait->mean,
@@ -907,6 +910,7 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
   if (!env || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
   if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
+  GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
 #define SAMPLE_REG(V_, NC_, NAV_, NP_)                                                   \
   if (launch_sample_reg<V_, NC_, NAV_, NP_>(c, env_bufs(env), eps, t, *bufs, (hipStream_t)stream)) { \
@@ -937,6 +941,7 @@ int mhppo_eval_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_ml
     return set_error(MHPPO_EINVAL, "choice actor must be %d -> 2", choice_dim(c));
   if (t < 0 || t >= bufs->T || t >= c.max_episode)
     return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T < c.max_episode ? bufs->T : c.max_episode);
+  GUARD_DEVICE(env_device(env));
   size_t shm = sizeof(float) * (2 * mlp_size(NF_C, 1) + mlp_size(choice_dim(c), 2));
   VLAUNCH(k_eval_step, c.variant, grid_for(c.N), shm, (hipStream_t)stream, c, env_bufs(env), *actor_cross,
           *actor_wait, *actor_choice, t, *bufs);
@@ -987,8 +992,8 @@ int mhppo_returns_scan_tm(const double *rew, float *ret, int64_t B, int32_t T, d
 }
 
 int mhppo_adv_stats(const float *ret, const float *value, int64_t M, double *stats, void *stream) {
+  if (M == 0) return MHPPO_OK;  // an empty shard (data parallel) adds nothing; its pointers may be NULL
   if (!ret || !value || !stats || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
-  if (M == 0) return MHPPO_OK;
   dim3 g = grid_for(M);
   double *part = scratch(2 * (size_t)g.x);
   if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
@@ -1001,8 +1006,8 @@ int mhppo_adv_stats(const float *ret, const float *value, int64_t M, double *sta
 
 int mhppo_adv_normalize(const float *ret, const float *value, int64_t M, const double *stats, double m_global,
                         float *adv, void *stream) {
-  if (!ret || !value || !stats || !adv || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (M == 0) return MHPPO_OK;
+  if (!ret || !value || !stats || !adv || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   hipLaunchKernelGGL(k_adv_norm, grid_for(M), dim3(TPB), 0, (hipStream_t)stream, ret, value, M, stats, m_global,
                      adv);
   CHECK_HIP(hipGetLastError());
@@ -1011,8 +1016,8 @@ int mhppo_adv_normalize(const float *ret, const float *value, int64_t M, const d
 
 int mhppo_ppo_cont_fwd_bwd(const float *mu, const float *act, const float *logp_old, const float *adv, int64_t M,
                            double inv_m, float *dmu, double *loss, void *stream) {
-  if (!mu || !act || !logp_old || !adv || !dmu || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (M == 0) return MHPPO_OK;
+  if (!mu || !act || !logp_old || !adv || !dmu || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   dim3 g = grid_for(M);
   double *part = scratch(g.x);
   if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
@@ -1025,9 +1030,9 @@ int mhppo_ppo_cont_fwd_bwd(const float *mu, const float *act, const float *logp_
 
 int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const float *adv, int64_t M,
                              const double *counts, double inv_m2, float *dprobs, double *loss, void *stream) {
+  if (M == 0) return MHPPO_OK;
   if (!probs || !logp_old || !adv || !counts || !dprobs || !loss || M < 0)
     return set_error(MHPPO_EINVAL, "bad argument");
-  if (M == 0) return MHPPO_OK;
   dim3 g = grid_for(M);
   double *part = scratch(g.x);
   if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
@@ -1040,8 +1045,8 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
 
 int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv, double *loss,
                       void *stream) {
-  if (!value || !ret || !dv || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (M == 0) return MHPPO_OK;
+  if (!value || !ret || !dv || !loss || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
   dim3 g = grid_for(M);
   double *part = scratch(g.x);
   if (!part) return set_error(MHPPO_ENOMEM, "scratch allocation failed");

@@ -122,7 +122,10 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def stream_ptr(stream=None):
+def stream_ptr(stream=None, device=None):
+    """hipStream_t of `stream`, else of the current stream of `device` (default: the
+    current device).  Handle-bound calls pass their handle's device: the library makes
+    that device current for the call (include/mhppo.h), so the stream must live there."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return ctypes.c_void_p(s.cuda_stream)

@@ -94,7 +94,7 @@ class VecCrosswalk:
 
     def reset(self, want_obs=True):
         obs = self._t((self.n_envs, self.obs_dim), torch.float32) if want_obs else None
-        _lib.check(_lib.lib().mhppo_env_reset(self._h, _lib.ptr(obs), _lib.stream_ptr()))
+        _lib.check(_lib.lib().mhppo_env_reset(self._h, _lib.ptr(obs), _lib.stream_ptr(device=self.device)))
         return obs
 
     def step(self, actions, want_obs=True):
@@ -107,19 +107,19 @@ class VecCrosswalk:
         rl = self._t((self.n_envs, self.n_reward_slots), torch.float64)
         done = self._t((self.n_envs,), torch.uint8)
         _lib.check(_lib.lib().mhppo_env_step(self._h, _lib.ptr(a), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(rl),
-                                             _lib.ptr(done), _lib.stream_ptr()))
+                                             _lib.ptr(done), _lib.stream_ptr(device=self.device)))
         return obs, rew, rl, done.bool()
 
     def get_state(self):
         """[N, state_dim] float64: per ped 20, per car slot 8, cross, time, ped_traffic, car_traffic, ped exist."""
         out = self._t((self.n_envs, self.state_dim), torch.float64)
-        _lib.check(_lib.lib().mhppo_env_get_state(self._h, _lib.ptr(out), _lib.stream_ptr()))
+        _lib.check(_lib.lib().mhppo_env_get_state(self._h, _lib.ptr(out), _lib.stream_ptr(device=self.device)))
         return out
 
     def get_rng(self):
         mt = self._t((self.n_envs, 624), torch.int32)
         mti = self._t((self.n_envs,), torch.int32)
-        _lib.check(_lib.lib().mhppo_env_get_rng(self._h, _lib.ptr(mt), _lib.ptr(mti), _lib.stream_ptr()))
+        _lib.check(_lib.lib().mhppo_env_get_rng(self._h, _lib.ptr(mt), _lib.ptr(mti), _lib.stream_ptr(device=self.device)))
         return mt, mti
 
     # ------------------------------------------------------------ checkpoint
@@ -134,7 +134,7 @@ class VecCrosswalk:
         L = _lib.lib()
         n = int(L.mhppo_env_state_bytes(self._h))
         blob = torch.empty(n, dtype=torch.uint8, device=self.device)
-        _lib.check(L.mhppo_env_export(self._h, _lib.ptr(blob), _lib.stream_ptr()))
+        _lib.check(L.mhppo_env_export(self._h, _lib.ptr(blob), _lib.stream_ptr(device=self.device)))
         return {"cfg": self._cfg_key(), "blob": blob.cpu()}
 
     def load_state_dict(self, sd):
@@ -144,5 +144,10 @@ class VecCrosswalk:
         blob = sd["blob"].to(device=self.device, dtype=torch.uint8).contiguous()
         if blob.numel() != int(L.mhppo_env_state_bytes(self._h)):
             raise ValueError("env checkpoint size mismatch")
-        _lib.check(L.mhppo_env_import(self._h, _lib.ptr(blob), _lib.stream_ptr()))
+        _lib.check(L.mhppo_env_import(self._h, _lib.ptr(blob), _lib.stream_ptr(device=self.device)))
         torch.cuda.current_stream(self.device).synchronize()
+
+    def device_scope(self):
+        """Context making the handle's device current (torch allocations and the ppo kernels,
+        which take no handle, then run on it)."""
+        return torch.cuda.device(self.device)

@@ -75,7 +75,8 @@ def k_adv_stats(ret, value):
     """(sum A, sum A^2) over local rows, float64 [2]."""
     stats = torch.zeros(2, dtype=torch.float64, device=ret.device)
     v = value.detach().contiguous()
-    _lib.check(_lib.lib().mhppo_adv_stats(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
+    with torch.cuda.device(ret.device):
+        _lib.check(_lib.lib().mhppo_adv_stats(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
                                           _lib.stream_ptr()))
     return stats
 
@@ -83,7 +84,8 @@ def k_adv_stats(ret, value):
 def k_adv_normalize(ret, value, stats, m_global):
     adv = torch.empty_like(ret)
     v = value.detach().contiguous()
-    _lib.check(_lib.lib().mhppo_adv_normalize(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
+    with torch.cuda.device(ret.device):
+        _lib.check(_lib.lib().mhppo_adv_normalize(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
                                               float(m_global), _lib.ptr(adv), _lib.stream_ptr()))
     return adv
 
@@ -92,7 +94,8 @@ def k_mse(value, ret, m_global):
     dv = torch.empty_like(ret)
     loss = torch.zeros(1, dtype=torch.float64, device=ret.device)
     v = value.detach().contiguous()
-    _lib.check(_lib.lib().mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global, _lib.ptr(dv),
+    with torch.cuda.device(ret.device):
+        _lib.check(_lib.lib().mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global, _lib.ptr(dv),
                                             _lib.ptr(loss), _lib.stream_ptr()))
     return dv, loss
 
@@ -101,7 +104,8 @@ def k_ppo_cont(mu, act, logp_old, adv, m_global):
     dmu = torch.empty_like(adv)
     loss = torch.zeros(1, dtype=torch.float64, device=adv.device)
     m = mu.detach().contiguous()
-    _lib.check(_lib.lib().mhppo_ppo_cont_fwd_bwd(_lib.ptr(m), _lib.ptr(act), _lib.ptr(logp_old), _lib.ptr(adv),
+    with torch.cuda.device(adv.device):
+        _lib.check(_lib.lib().mhppo_ppo_cont_fwd_bwd(_lib.ptr(m), _lib.ptr(act), _lib.ptr(logp_old), _lib.ptr(adv),
                                                  adv.numel(), 1.0 / m_global, _lib.ptr(dmu), _lib.ptr(loss),
                                                  _lib.stream_ptr()))
     return dmu, loss
@@ -111,7 +115,8 @@ def k_ppo_choice(probs, logp_old, adv, counts, m_global):
     p = probs.detach().contiguous()
     dp = torch.empty_like(p)
     loss = torch.zeros(1, dtype=torch.float64, device=adv.device)
-    _lib.check(_lib.lib().mhppo_ppo_choice_fwd_bwd(_lib.ptr(p), _lib.ptr(logp_old), _lib.ptr(adv), adv.numel(),
+    with torch.cuda.device(adv.device):
+        _lib.check(_lib.lib().mhppo_ppo_choice_fwd_bwd(_lib.ptr(p), _lib.ptr(logp_old), _lib.ptr(adv), adv.numel(),
                                                    _lib.ptr(counts), 1.0 / (m_global * m_global), _lib.ptr(dp),
                                                    _lib.ptr(loss), _lib.stream_ptr()))
     return dp, loss
@@ -169,9 +174,10 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     if TRAIN_EVENTS is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    _lib.check(_lib.lib().mhppo_mlp_train(
-        kind, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts), float(m_global),
-        float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().mhppo_mlp_train(
+            kind, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts),
+            float(m_global), float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
     if ev is not None:
         ev[1].record()
         TRAIN_EVENTS.append((kind, net.n_in, M, ev[0], ev[1]))

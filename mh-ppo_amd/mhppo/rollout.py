@@ -89,7 +89,7 @@ class RolloutGPU:
         mc, tc = actor_cross.mlp_desc()
         mw, tw = actor_wait.mlp_desc()
         md, td = actor_choice.mlp_desc()
-        st = _lib.stream_ptr()
+        st = _lib.stream_ptr(device=venv.device)
         for _ in range(episodes):
             R = dict(obs_hist=z((T, N, venv.obs_dim), torch.float32), acts=z((T, N, S), torch.float32),
                      rews_c=z((T, N, S), torch.float32), rews_d=z((T, N, S), torch.float32),
@@ -117,7 +117,7 @@ class RolloutGPU:
         L = _lib.lib()
         key = (int(seed) * 1000003 + int(iteration)) & 0xFFFFFFFFFFFFFFFF
         off = int(self.venv.cfg.env_id_offset)
-        st = _lib.stream_ptr()
+        st = _lib.stream_ptr(device=self.venv.device)
         _lib.check(L.mhppo_philox_uniform(key, off * self.S * self.P, _lib.ptr(self.u), self.u.numel(), st))
         # step t's normals from counters (t + 1) * 2^40 + global (env, slot): one launch
         _lib.check(L.mhppo_philox_normal_2d(key, _CTR_STEP + off * self.S, _CTR_STEP, _lib.ptr(self.eps), self.T,
@@ -138,7 +138,7 @@ class RolloutGPU:
         mc, tc = actor_choice.mlp_desc()
         mx, tx = actor_cross.mlp_desc()
         mw, tw = actor_wait.mlp_desc()
-        st = _lib.stream_ptr()
+        st = _lib.stream_ptr(device=self.venv.device)
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
         for t in range(self.T):

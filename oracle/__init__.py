@@ -118,6 +118,97 @@ class OracleEnv:
         return mt, int(mti[0])
 
 
+def set_threads(n=0):
+    """OpenMP threads of the batch oracle (0 = leave as is); returns the current count."""
+    L = lib()
+    L.oracle_set_threads.restype = ctypes.c_int
+    L.oracle_set_threads.argtypes = [ctypes.c_int]
+    return L.oracle_set_threads(int(n))
+
+
+class OracleBatch:
+    """N oracle envs (env e seeded seed_base + e), stepped with OpenMP over envs
+    (batch_oracle.c).  Same per-env code as OracleEnv."""
+
+    def __init__(self, variant, n, nb_car, nb_ped, nb_lines, seed_base=0, dt=0.3, max_episode=80, sin=True,
+                 flags=0):
+        L = lib()
+        P_, I, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        L.oracle_batch_create.restype = P_
+        L.oracle_batch_create.argtypes = [I, I, I, I, I, D, I, I, P_, P_, P_, ctypes.c_uint64, I]
+        L.oracle_batch_destroy.argtypes = [P_]
+        L.oracle_batch_obs_dim.restype = I
+        L.oracle_batch_obs_dim.argtypes = [P_]
+        L.oracle_batch_dump_dim.restype = I
+        L.oracle_batch_dump_dim.argtypes = [P_]
+        L.oracle_batch_reset.argtypes = [P_, P_]
+        L.oracle_batch_step.argtypes = [P_] * 8
+        L.oracle_batch_get_rng.argtypes = [P_] * 3
+        L.oracle_batch_rollout.argtypes = [P_, I, P_, P_, P_, ctypes.c_float, ctypes.c_float] + [P_] * 14
+        self.variant, self.n = variant, n
+        self.nb_car, self.nb_ped, self.nb_lines = nb_car, nb_ped, nb_lines
+        self.S = 2 * nb_lines if variant == "scalable" else nb_car
+        self._cb = np.ascontiguousarray(CAR_B, dtype=np.float64)
+        self._pb = np.ascontiguousarray(PED_B, dtype=np.float64)
+        self._xb = np.ascontiguousarray(CROSS_B, dtype=np.float64)
+        self.h = L.oracle_batch_create(VARIANTS[variant], n, nb_car, nb_ped, nb_lines, dt, max_episode, int(sin),
+                                       _p(self._cb), _p(self._pb), _p(self._xb), seed_base, int(flags))
+        if not self.h:
+            raise ValueError("oracle_batch_create rejected the shape")
+        self.obs_dim = L.oracle_batch_obs_dim(self.h)
+        self.dump_dim = L.oracle_batch_dump_dim(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_batch_destroy(self.h)
+            self.h = None
+
+    def reset(self):
+        o = np.zeros((self.n, self.obs_dim), np.float32)
+        lib().oracle_batch_reset(self.h, _p(o))
+        return o
+
+    def step(self, actions, want_dump=False):
+        """-> obs, rewards, reward_light, done, dump (or None), mti (RNG cursor after the step)."""
+        a = np.ascontiguousarray(actions, dtype=np.float64)
+        assert a.shape == (self.n, 2 * self.S)
+        o = np.zeros((self.n, self.obs_dim), np.float32)
+        r = np.zeros((self.n, self.S), np.float64)
+        rl = np.zeros((self.n, self.S), np.float64)
+        d = np.zeros(self.n, np.uint8)
+        dm = np.zeros((self.n, self.dump_dim), np.float64) if want_dump else None
+        mti = np.zeros(self.n, np.int32)
+        lib().oracle_batch_step(self.h, _p(a), _p(o), _p(r), _p(rl), _p(d), None if dm is None else _p(dm), _p(mti))
+        return o, r, rl, d.astype(bool), dm, mti
+
+    def rng_state(self):
+        mt = np.zeros((self.n, 624), np.uint32)
+        mti = np.zeros(self.n, np.int32)
+        lib().oracle_batch_get_rng(self.h, _p(mt), _p(mti))
+        return mt, mti
+
+    def rollout(self, w_cross, w_wait, w_choice, mean=-1.0, std=3.0, forced_a=None, u=None, eps=None, T=80):
+        """One Env_rollout.iterations_rand episode per env, outputs as oracle.rollout();
+        eps float32 [T, n, S] (the GPU's layout)."""
+        n, S, P = self.n, self.S, self.nb_ped
+        dc = choice_dim(self.variant, S)
+        out = dict(feat_d=np.zeros((n, S, P, dc), np.float32), probs_d=np.zeros((n, S, P, 2), np.float32),
+                   a_d=np.zeros((n, S, P), np.int32), logp_d=np.zeros((n, S, P), np.float32),
+                   closest=np.zeros((n, S), np.int32), exist=np.zeros((n, S), np.uint8),
+                   obs_c=np.zeros((n, S, T, 13), np.float32), act=np.zeros((n, S, T), np.float32),
+                   logp=np.zeros((n, S, T), np.float32), rew=np.zeros((n, S, T), np.float64),
+                   ep_min=np.zeros((n, S), np.float64))
+        wc, ww, wd = (np.ascontiguousarray(w, np.float32) for w in (w_cross, w_wait, w_choice))
+        ep = np.ascontiguousarray(np.asarray(eps, np.float32).transpose(1, 0, 2))  # [n, T, S]
+        uu = np.ascontiguousarray(u if u is not None else np.zeros((n, S, P)), np.float32)
+        fa = None if forced_a is None else np.ascontiguousarray(forced_a, np.int32)
+        lib().oracle_batch_rollout(self.h, T, _p(wc), _p(ww), _p(wd), mean, std, None if fa is None else _p(fa),
+                                   _p(uu), _p(ep), *[_p(out[k]) for k in (
+                                       "feat_d", "probs_d", "a_d", "logp_d", "closest", "exist", "obs_c", "act",
+                                       "logp", "rew", "ep_min")])
+        return out
+
+
 def rng_stream(seed, kind, n, a=0.0, b=0.0, per=1):
     L = lib()
     L.oracle_rng_stream.restype = ctypes.c_int
@@ -239,9 +330,13 @@ def _mlp(n_in, n_out, kind):
     return _M()
 
 
-def cpu_iteration(variant, n, nb_car, nb_ped, nb_lines, seed=0):
-    """One full PPO iteration on the CPU: C oracle env + rollout for n envs (1 thread),
-    then 10+10 epochs of the PyTorch-CPU update restatement (oracle/ppo_ref.py)."""
+def cpu_iteration(variant, n, nb_car, nb_ped, nb_lines, seed=0, timings=None):
+    """One full PPO iteration on the CPU: C oracle env + rollout for n envs (OpenMP over
+    envs, set_threads), then 10+10 epochs of the PyTorch-CPU update restatement
+    (oracle/ppo_ref.py, torch's intra-op threads).  timings (dict or None) accumulates
+    the seconds of the 'rollout' and 'update' legs."""
+    import time
+
     import torch
     from . import ppo_ref
     S = 2 * nb_lines if variant == "scalable" else nb_car
@@ -257,8 +352,10 @@ def cpu_iteration(variant, n, nb_car, nb_ped, nb_lines, seed=0):
     rng = np.random.default_rng(seed)
     eps = rng.normal(size=(80, n, S)).astype(np.float32)
     u = rng.uniform(size=(n, S, nb_ped)).astype(np.float32)
-    o = rollout(variant, nb_car, nb_ped, nb_lines, [seed * n + e for e in range(n)], nets["ac"].packed(),
-                nets["aw"].packed(), nets["ad"].packed(), u=u, eps=eps)
+    t0 = time.perf_counter()
+    ob = OracleBatch(variant, n, nb_car, nb_ped, nb_lines, seed_base=seed * n)
+    o = ob.rollout(nets["ac"].packed(), nets["aw"].packed(), nets["ad"].packed(), u=u, eps=eps)
+    t1 = time.perf_counter()
     action_d_i = 2 * o["a_d"].reshape(n, -1)[:, :S] - 1
     ex = o["exist"].astype(bool) if variant == "scalable" else np.ones((n, S), bool)
     ret = ppo_ref.returns_scan(torch.tensor(o["rew"].reshape(-1, 80))).reshape(n, S, 80)
@@ -281,4 +378,7 @@ def cpu_iteration(variant, n, nb_car, nb_ped, nb_lines, seed=0):
     for _ in range(10):
         ppo_ref.train_model_d(nets["ad"], nets["cd"], opts["ad"], opts["cd"], torch.tensor(fd), torch.tensor(ad_),
                               torch.tensor(lpd), torch.tensor(rd))
+    if timings is not None:
+        timings["rollout"] = timings.get("rollout", 0.0) + (t1 - t0)
+        timings["update"] = timings.get("update", 0.0) + (time.perf_counter() - t1)
     return n * 80

@@ -3,8 +3,8 @@
 Bit-exact: RNG streams (final MT19937 state), done flags, every discrete field of
 the internal state, observations.  Float64 rewards / reward_light / continuous
 state: device libm (ocml exp/pow/log/sin/cos) may differ from glibc by an ulp,
-so those are checked to 1e-9 relative — and the count of non-identical values is
-reported, the fraction is small.
+so those are checked to 1e-9 relative, and at most 2 % of them may differ in their
+last bits (0.47-0.77 % measured on 65 536 envs x 80 steps, test_env_fullscale_gpu.py).
 """
 import glob
 import os
@@ -73,7 +73,9 @@ def test_gpu_env_matches_oracle_many_envs(case):
         np.testing.assert_allclose(rl, rrl, rtol=1e-9, atol=1e-12)
         n_diff += int((r != rr).sum() + (rl != rrl).sum())
         n_tot += r.size + rl.size
-    assert n_diff <= 0.2 * n_tot, f"{n_diff}/{n_tot} float64 outputs differ by more than rounding"
+    # measured at full scale (tests/test_env_fullscale_gpu.py, profiles/r02_parity_fullscale): 0.47-0.77 % of
+    # the float outputs differ in their last bits (device libm vs glibc), none diverges discretely
+    assert n_diff <= 0.02 * n_tot, f"{n_diff}/{n_tot} float64 outputs differ in their last bits"
 
 
 @pytest.mark.parametrize("case", [("coop", 2, 1, 2), ("4cars", 4, 1, 2), ("scalable", 8, 1, 4), ("stop", 2, 1, 2),
