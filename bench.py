@@ -1,54 +1,61 @@
 #!/usr/bin/env python3
 """MH-PPO hot-path benchmark on MI355X (driver contract: see task README).
 
-One bench "step" = one full PPO iteration on this rank's shard:
-    reset N envs -> 80 rollout steps (choice head at t=0; per step: policy
-    kernel + fused sample/env-step kernel) -> returns scan -> bucketing ->
-    10 epochs (cross, wait) + 10 epochs (choice) of full-batch PPO updates.
-Workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
-    Env_hybrid_multi_coop_4cars, 4 AVs (+4 IDM followers), 1 pedestrian,
-    2 lanes, 65536 envs per GPU (weak scaling over ranks), T = 80.
+One bench "step" = one full PPO iteration on this rank's shard, exactly Algo_PPO.train's
+loop body (Coop-MH-PPO-scalable.py:854-917):
+    rollout.reset() -> reset N envs + 80 rollout steps (choice head at t=0; per step:
+    policy kernel + fused sample/env-step kernel) -> returns scan -> bucketing ->
+    10 joint epochs of the three heads (cross, wait, choice) -> rollout.reset().
+Default workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
+    Env_hybrid_multi_coop_4cars, 4 AVs (+4 IDM followers), 1 pedestrian, 2 lanes,
+    65536 envs per GPU (weak scaling over ranks), T = 80.
+    `--config 4`: Env_hybrid_multi_coop_scalable 8/1/4, ragged 1-8 agents (configs[3]).
 value = (all ranks' envs) * 80 env-steps / max-over-ranks iteration time.
 
+Multi-GPU: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
+starts N ranks itself (torch.distributed.run, one process per GPU, RCCL) before this
+process touches the GPU, and relays rank 0's JSON line; under an external launcher
+(WORLD_SIZE set) it is one rank.  Envs shard by global id: rank r owns env ids
+[r*N, (r+1)*N).
+
 Extra JSON fields:
-  roofline     — the dominant kernel, the fused continuous-head train kernel
-                 (mhppo_mlp_train_cont, ~60 % of GPU time): algorithmic FLOPs per
-                 row x rows / launch duration, from HIP events on
-                 its stream inside the timed region, summed over all launches;
-                 f32 MFMA peak 157.3 TFLOP/s (exact-f32 matrix rate on gfx950).
-  roofline_env — the fused sample+env-step kernel (mhppo_rollout_sample_env):
-                 algorithmic bytes per env-step x N / its mean duration; 8 TB/s.
-  cpu_baseline — the C oracle (same env + rollout, glibc) + PyTorch-CPU update
-                 on a bounded sample of the same workload, rank 0, N=1 only.
+  roofline     — the dominant kernel, the fused continuous-head train kernel (k_mlp_train,
+                 ~85 % of GPU time): algorithmic FLOPs per row x rows /
+                 launch duration, from HIP events on its stream inside the timed region,
+                 summed over all launches; f32 MFMA peak 157.3 TFLOP/s.
+  roofline_env — the fused sample+env-step kernel: SURVEY §8(d)'s algorithmic bytes per
+                 env-step (cfg3 1515 B, cfg4 1615 B) x N / its mean duration; 8 TB/s.
+  cpu_baseline — the C oracle (same env + rollout, glibc, OpenMP over envs on the box's
+                 cores) + the PyTorch-CPU update (same thread count) on a bounded sample
+                 of the same workload, rank 0, N=1 only; legs timed separately.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec at 65536 envs × 4 agents, 1/2/4/8 MI355X + %HBM roofline"
 HBM_PEAK_GBS = 8000.0
 F32_MFMA_PEAK_TFLOPS = 157.3
+CONFIGS = {3: ("4cars", 4, 1, 2), 4: ("scalable", 8, 1, 4), 2: ("coop", 2, 1, 2)}
 
 
-def env_step_bytes(S, nC, P, obs_dim, T=80):
-    """Algorithmic HBM bytes one env moves in one fused sample+env-step launch.
-    With one pedestrian the policy kernel writes the step's feature record in place
-    (include/mhppo.h), so this kernel neither reads feat_c nor writes obs_c."""
-    car = nC * 11 * 8 + nC * 6 * 8 + S * 3 * 8      # read 11 fields/car, write 6 dynamic (+3 detection fields per AV)
-    ped = P * (17 * 8 + 4) + P * (10 * 8 + 4)      # read 17 f64 + flags, write 10 dynamic f64 + flags
-    env = 8 + 8 + 4 + 4 + 4 + 4 + 8               # cross, time r/w, mti r/w, block bits, ped_traffic, RNG words
-    feat = 0 if P == 1 else 2 * S * 13 * 4          # selected feature row: read feat_c, write obs_c
-    io_in = S * P * 4 + S * 4 + S * P * 4 + S * 4 + S * 8   # out_c, eps, a_d, closest, ep_min
-    io_out = S * 4 + S * 4 + S * 8 + S * 8 + obs_dim * 4     # act, logp, rew, ep_min, obs
-    return car + ped + env + feat + io_in + io_out
+def env_step_bytes(S, P, A_ctl, obs_dim):
+    """algorithmic HBM bytes of one env-step of the step kernel —
+    dynamic state read + written in fp64 (car 56 B, ped 88 B, env 12 B), static state
+    read once (car 2 B, ped 78 B, env 12 B), actions 2 A_ctl floats in, obs_dim floats
+    + rewards/reward_light (8 A_ctl) + done out, 8 B of RNG words.
+    cfg3 (S 8, P 1, A 4, obs 60): 1515 B; cfg4 (S 8, P 1, A 8, obs 69): 1615 B."""
+    return 2 * (S * 56 + P * 88 + 12) + (S * 2 + P * 78 + 12) + 4 * 2 * A_ctl + 4 * obs_dim + 8 * A_ctl + 1 + 8
 
 
 def pmc_traffic(*patterns):
@@ -71,46 +78,68 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                    help="BASELINE.json config: 3 = 4cars 4/1/2 (the metric), 4 = scalable 8/1/4, 2 = coop 2/1/2")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--variant", default="4cars")
-    ap.add_argument("--nb-car", type=int, default=4)
-    ap.add_argument("--nb-ped", type=int, default=1)
-    ap.add_argument("--nb-lines", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-envs", type=int, default=256)
+    ap.add_argument("--cpu-sample-envs", type=int, default=4096)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--save-nets", default=None, help="rank 0 saves every net's flat weights here (tests)")
     return ap.parse_args()
 
 
-def cpu_baseline(a, seconds_cap=30.0):
-    """Oracle rollout (C, glibc) + PyTorch-CPU PPO update on a bounded env sample."""
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """Start `--gpus` ranks (one process per GPU) as children and relay their output.
+    Runs before this process makes any GPU call; returns the children's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_baseline(a, variant, nc, npd, nl):
+    """Oracle env + rollout (C, glibc, OpenMP over envs) + PyTorch-CPU update on a bounded
+    sample of the same workload: one untimed small iteration, then one timed iteration of
+    `--cpu-sample-envs` envs (10-30 s of CPU work on the box's share of cores)."""
     try:
-        from oracle import cpu_iteration
+        import oracle
     except Exception as ex:  # pragma: no cover - reported, never silently substituted
         return {"value": None, "unit": "env-steps/s", "cores": 0, "kind": "port", "sample": f"unavailable: {ex}"}
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    oracle.set_threads(threads)
     torch.set_num_threads(threads)
+    oracle.cpu_iteration(variant, 64, nc, npd, nl, seed=999)  # warm caches / torch CPU init (untimed)
     n = a.cpu_sample_envs
+    tm = {}
     t0 = time.perf_counter()
-    iters = 0
-    while True:
-        cpu_iteration(a.variant, n, a.nb_car, a.nb_ped, a.nb_lines, seed=iters)
-        iters += 1
-        if time.perf_counter() - t0 > min(seconds_cap, 10.0) or iters >= 3:
-            break
-    dt = (time.perf_counter() - t0) / iters
+    oracle.cpu_iteration(variant, n, nc, npd, nl, seed=0, timings=tm)
+    dt = time.perf_counter() - t0
     return {"value": n * 80 / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs x 80 steps x {iters} iterations (oracle env+rollout in C, 1 thread; "
-                      f"update PyTorch-CPU {threads} threads), {dt:.2f} s/iteration"}
+            "sample": f"{n} envs x 80 steps, 1 full iteration (C oracle env+rollout, OpenMP {threads} threads: "
+                      f"{tm['rollout']:.2f} s = {n * 80 / tm['rollout']:.0f} env-steps/s; PyTorch-CPU update "
+                      f"10+10 epochs, {threads} threads: {tm['update']:.2f} s), {dt:.2f} s total",
+            "rollout_s": tm["rollout"], "update_s": tm["update"], "threads_rollout": threads,
+            "threads_update": threads}
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one GPU per rank; with fewer GPUs than ranks (a rehearsal) ranks share them round-robin
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    # one GPU per rank; with fewer GPUs than ranks (a gloo rehearsal) ranks share them round-robin
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
@@ -118,27 +147,30 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(a.dist_backend)
+    from mhppo import ppo
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
-    from mhppo import ppo
 
+    variant, nc, npd, nl = CONFIGS[a.config]
     N, T = a.envs, 80
-    venv = VecCrosswalk(a.variant, N, a.nb_car, a.nb_ped, a.nb_lines, seed_base=0, env_id_offset=rank * N,
-                        device=f"cuda:{local}")
+    venv = VecCrosswalk(variant, N, nc, npd, nl, seed_base=0, env_id_offset=rank * N, device=f"cuda:{local}")
     torch.manual_seed(0)
     algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
+    ro = algo.rollout
 
     def iteration(events=None):
-        algo.rollout.reset()
+        """Algo_PPO.train's loop body (mhppo/algo.py), with the env-step kernel bracketed."""
+        ro.reset()
         with torch.no_grad():
-            algo.rollout.batch = algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait,
-                                                          algo.actor_net_choice, seed=0,
-                                                          iteration=algo.rollout.iteration, step_events=events)
-        algo.rollout.iteration += 1
+            ro.batch = ro.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
+                                      iteration=ro.iteration, step_events=events)
+        ro.iteration += 1
         from mhppo.rollout import bucket_segments
-        algo.rollout.cross, algo.rollout.wait, algo.rollout.choice = bucket_segments(algo.rollout.batch)
+        ro.cross, ro.wait, ro.choice = bucket_segments(ro.batch)
+        ro.gpu.check()
         algo.update()
+        ro.reset()
 
     for _ in range(a.warmup):
         iteration()
@@ -163,8 +195,8 @@ def main():
     value = world * N * T / (dt / a.steps)
     kern_ms = sum(ev[0].elapsed_time(ev[1]) for evs in events for ev in evs) / (a.steps * T)
     S = venv.n_slots
-    nC = 2 * S if a.variant == "4cars" else S
-    per_env = env_step_bytes(S, nC, a.nb_ped, venv.obs_dim)
+    S_all = 2 * S if variant == "4cars" else S  # car slots incl. the 4cars IDM followers
+    per_env = env_step_bytes(S_all, npd, S, venv.obs_dim)
     achieved = per_env * N / (kern_ms * 1e-3) / 1e9
     tr = [e for e in ppo.TRAIN_EVENTS if e[1] == 13]  # the continuous heads' launches
     ppo.TRAIN_EVENTS = None
@@ -174,14 +206,17 @@ def main():
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic = pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>")
     traffic_env = pmc_traffic("k_sample_env")
+    agents = "ragged 1-8 existing of 8 slots" if variant == "scalable" else S
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64 env / f32 nets", "data": "synthetic (random-init Model_PPO heads, CPython-MT19937 env streams, "
                                             "Philox policy noise)",
-        "config": {"workload": f"{a.variant} nb_car={a.nb_car} nb_ped={a.nb_ped} nb_lines={a.nb_lines}, "
-                               f"{N} envs/GPU x 80 steps, full PPO iteration (rollout + returns + 10+10 epochs)",
-                   "envs_per_gpu": N, "agents": S, "T": T, "parallelism": f"dp{world}"},
+        "config": {"workload": f"config {a.config}: {variant} nb_car={nc} nb_ped={npd} nb_lines={nl}, {N} envs/GPU x "
+                               f"80 steps, full PPO iteration (rollout + returns + 10+10 epochs)",
+                   "envs_per_gpu": N, "agents": agents, "T": T, "parallelism": f"dp{world}"},
+        "dist": {"world_size": world, "backend": (a.dist_backend if world > 1 else None),
+                 "env_ranges": [[r * N, (r + 1) * N] for r in range(world)]},
         "roofline": {"bound": "mfma", "kernel": "k_mlp_train (fused continuous-head fwd/loss/bwd/wgrad, f32 MFMA)",
                      "achieved": tr_tflops, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tr_tflops / F32_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "B/launch",
@@ -191,13 +226,17 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_env, "traffic_unit": "B/launch",
                          "bytes_per_launch": per_env * N, "bytes_per_env_step": per_env,
-                         "kernel_ms": kern_ms},
+                         "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3)},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(a)
+        line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)
+    if rank == 0 and a.save_nets:
+        import numpy as np
+        np.save(a.save_nets, np.concatenate([net.flat().cpu().numpy() for net in algo.nets()]))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -25,6 +25,8 @@ extern "C" {
 #define MHPPO_EINVAL -1   /* invalid configuration / argument */
 #define MHPPO_EHIP -2     /* HIP runtime error */
 #define MHPPO_ENOMEM -3   /* device allocation failed */
+#define MHPPO_ENAN -4     /* NaN policy output: the reference raises ValueError from torch.distributions'
+                             argument validation (Categorical probs / MultivariateNormal loc) */
 
 /* Env variants = the reference gym ids (Environments/__init__.py:3-42). */
 #define MHPPO_COOP 0      /* Crosswalk_hybrid_multi_coop-v0          Env_hybrid_multi_coop.py:625 */
@@ -138,6 +140,8 @@ typedef struct mhppo_rollout_bufs {
     uint8_t *exist;
     int32_t *rows;
     int32_t T, flags;   /* flags: MHPPO_ROLLOUT_* */
+    uint32_t *status;   /* optional device word (caller zeroes it): bit 0 = a NaN choice probability,
+                           bit 1 = a NaN continuous action mean was sampled; see mhppo_rollout_check */
 } mhppo_rollout_bufs;
 /* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
  * instead of the MFMA kernel; both are bit-identical (A/B and tests) */
@@ -188,6 +192,12 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
                          mhppo_rollout_bufs *bufs, void *stream);
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
 
+/* Status of the rollout launches queued on `stream` so far: synchronises the stream, reads
+ * and clears bufs->status, and returns MHPPO_ENAN when a NaN policy output was drawn from
+ * (Categorical(probs) at the episode start, :409; MultivariateNormal(loc) per step, :451:
+ * where the reference's torch.distributions raise ValueError), else MHPPO_OK. */
+int mhppo_rollout_check(mhppo_rollout_bufs *bufs, void *stream);
+
 /* Philox-4x32-10 noise (perf mode): out[i] for counter (offset + i) under key `seed`. */
 int mhppo_philox_normal(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
 int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, void *stream);
@@ -230,12 +240,12 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
 /* Fused training pass of one Model_PPO head (n_in -> 32 -> 64 -> 32 -> n_out) on f32 MFMA:
  * forward + loss gradient + backward + weight gradient over M rows, replacing the torch
  * GEMMs/autograd of one epoch of train_model_c (:778-815) / train_model_d (:818-851).
- * kind 0 = critic (n_in <= 32, n_out 1): writes value[M]; grad = dMSE/dW;
+ * kind 0 = critic (n_in <= 64, n_out 1): writes value[M]; grad = dMSE/dW;
  *          sums[0..2] += (sum (V-G)^2, sum A, sum A^2) with A = G - V.
  * kind 1 = continuous actor (n_in 13, n_out 1, tanh*out_std + out_mean): reads value[M],
  *          act, logp_old and the GLOBAL (sum A, sum A^2) in stats[0..1];
  *          grad = d(clip surrogate)/dW, sums[0] += sum of surrogate terms.
- * kind 2 = choice actor (n_in <= 32, n_out 2, pairwise softmax): reads value, logp_old,
+ * kind 2 = choice actor (n_in <= 64, n_out 2, pairwise softmax): reads value, logp_old,
  *          stats and the GLOBAL action counts counts[0..1] (float64);
  *          grad = d(O(M) Categorical surrogate / M_global^2)/dW, sums[0] += its sum.
  *          counts == NULL selects the opt-in per-row loss: act[M] (0/1 as

@@ -28,7 +28,8 @@
 //             pn = p / sum(p) normalisation and the clamp, then the softmax Jacobian.
 // Continuous heads (13 inputs, the big batches) run 8 waves per CU (2 per SIMD) with the
 // next tile's inputs prefetched into a double-buffered LDS slot by LDS-DMA; the other
-// instantiations (choice obs of 12..32 features, small batches) load synchronously.
+// instantiations (choice obs of 12..64 features, small batches) load synchronously; their
+// dW1 is one 32x32 tile per 32 input columns.
 // Outputs per wave: the packed torch-layout gradient and float64 partial sums;
 // k_grad_stage1/2 sum the per-wave partials in fixed order (deterministic).
 #include <hip/hip_runtime.h>
@@ -53,7 +54,8 @@ constexpr int TILE = 32 * ST;             // one transposed 32x32 tile
 __host__ __device__ constexpr int n_params(int nin, int nout) {
   return 32 * nin + 32 + 64 * 32 + 64 + 32 * 64 + 32 + nout * 32 + nout;
 }
-constexpr int NW_MAX = n_params(32, 2);
+constexpr int NIN_MAX = 64;  // choice heads: dc = 2 + 6(S-1) + 10 = 54 for the scalable 8-slot env
+constexpr int NW_MAX = n_params(NIN_MAX, 2);
 
 // LDS layout (floats) of one instantiation: KS = layer-1 k-steps (inputs padded to 2 KS),
 // PF = double-buffered DMA prefetch (13-input heads), NOUT = output width.
@@ -268,8 +270,9 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   const int j = l & 31;
   const int kh = l >> 5;
 
-  // persistent accumulators
-  f32x16 gW1 = zero16(), gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
+  // persistent accumulators (gW1b: input columns 32..63 of dW1, heads with n_in > 32)
+  constexpr bool W1B = !PF && 2 * KS > 32;
+  f32x16 gW1 = zero16(), gW1b = zero16(), gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
   // 13-input heads: dW1 = dH1^T X is [32 features x 14 columns] — two 16x16 tiles of the
   // 16x16x4 MFMA (half the cycles of one 32x32 tile); D row (l>>4)*4 + r, column l & 15
   f32x4 gW1q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -543,6 +546,14 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
         float b = (j < nin) ? Xs[k * nin + j] : ((FOLD_B1 && j == nin) ? 1.0f : 0.0f);
         gW1 = mfma(T0[j * ST + k], b, gW1);
       }
+      if constexpr (W1B) {
+#pragma unroll
+        for (int s = 0; s < 16; s++) {
+          int k = 2 * s + kh;
+          float b = (32 + j < nin) ? Xs[k * nin + 32 + j] : 0.0f;
+          gW1b = mfma(T0[j * ST + k], b, gW1b);
+        }
+      }
     }
     wave_sync();
     phase();
@@ -555,6 +566,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   for (int r = 0; r < 16; r++) {
     int f = feat(r, l);
     if (!PF && j < nin) gp[G_W1 + f * nin + j] = gW1[r];
+    if (W1B && 32 + j < nin) gp[G_W1 + f * nin + 32 + j] = gW1b[r];
     gp[G_W2 + f * 32 + j] = gW2a[r];
     gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
     gp[G_W3 + f * 64 + j] = gW3a[r];
@@ -668,8 +680,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
                                float *value, const float *act, const float *logp_old, const double *stats,
                                const double *counts, double m_global, float out_mean, float out_std, float *grad,
                                double *sums, void *stream) {
-  if (!grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 || n_in > 32)
-    return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= 32)");
+  if (!grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 || n_in > NIN_MAX)
+    return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= %d)", NIN_MAX);
   hipStream_t s = (hipStream_t)stream;
   if (M == 0) {  // an empty shard (data parallel): zero gradient, sums unchanged; X/ret/value may be NULL
     CHECK_HIP(hipMemsetAsync(grad, 0, sizeof(float) * n_params(n_in, kind == K_CHOICE ? 2 : 1), s));
@@ -717,16 +729,23 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     else
       launch<K_CONT, 7, true>(MLP_ARGS);
   } else {
-    const int ks = n_in <= 16 ? 8 : (n_in <= 24 ? 12 : 16);
-    if (kind == K_CRITIC) {
-      if (ks == 8) launch<K_CRITIC, 8, false>(MLP_ARGS);
-      else if (ks == 12) launch<K_CRITIC, 12, false>(MLP_ARGS);
-      else launch<K_CRITIC, 16, false>(MLP_ARGS);
-    } else {
-      if (ks == 8) launch<K_CHOICE, 8, false>(MLP_ARGS);
-      else if (ks == 12) launch<K_CHOICE, 12, false>(MLP_ARGS);
-      else launch<K_CHOICE, 16, false>(MLP_ARGS);
+    // layer-1 k-steps: inputs padded to 2 KS columns
+    const int ks = n_in <= 16 ? 8 : (n_in <= 24 ? 12 : (n_in <= 32 ? 16 : (n_in <= 48 ? 24 : (n_in <= 56 ? 28 : 32))));
+#define KS_CASES(KIND_)                                       \
+    switch (ks) {                                             \
+      case 8: launch<KIND_, 8, false>(MLP_ARGS); break;       \
+      case 12: launch<KIND_, 12, false>(MLP_ARGS); break;     \
+      case 16: launch<KIND_, 16, false>(MLP_ARGS); break;     \
+      case 24: launch<KIND_, 24, false>(MLP_ARGS); break;     \
+      case 28: launch<KIND_, 28, false>(MLP_ARGS); break;     \
+      default: launch<KIND_, 32, false>(MLP_ARGS); break;     \
     }
+    if (kind == K_CRITIC) {
+      KS_CASES(K_CRITIC)
+    } else {
+      KS_CASES(K_CHOICE)
+    }
+#undef KS_CASES
   }
 #undef MLP_ARGS
   const int np = n_params(n_in, kind == K_CHOICE ? 2 : 1);

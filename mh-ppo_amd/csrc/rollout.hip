@@ -68,6 +68,7 @@ __global__ void __launch_bounds__(TPB)
   float p0 = e0 / s, p1 = e1 / s;
   B.probs_d[r * 2] = p0;
   B.probs_d[r * 2 + 1] = p1;
+  if ((p0 != p0 || p1 != p1) && B.status) atomicOr(B.status, 1u);  // Categorical raises on NaN probs
   // Categorical(probs): normalise, clamp to [eps, 1-eps], log (torch/distributions/utils.py)
   float sum = p0 + p1;
   float n0 = p0 / sum, n1 = p1 / sum;
@@ -405,6 +406,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
       loc = t_minimum(loc, out);
       if (out == loc) sel = p;
     }
+    if (loc != loc && B.status) atomicOr(B.status, 2u);  // MultivariateNormal raises on a NaN loc
     float z = eps[(size_t)e * S + i];
     float a = loc + MVN_L * z;
     const size_t bt = ((size_t)t * c.N + e) * S + i;  // time-major records [T][N][S]
@@ -929,6 +931,20 @@ int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo
   int rc = mhppo_rollout_policy(env, actor_cross, actor_wait, bufs, stream);
   if (rc) return rc;
   return mhppo_rollout_sample_env(env, eps, t, bufs, stream);
+}
+
+int mhppo_rollout_check(mhppo_rollout_bufs *bufs, void *stream) {
+  if (!bufs) return set_error(MHPPO_EINVAL, "null argument");
+  if (!bufs->status) return MHPPO_OK;
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t st = 0;
+  CHECK_HIP(hipMemcpyAsync(&st, bufs->status, sizeof(st), hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  if (!st) return MHPPO_OK;
+  CHECK_HIP(hipMemsetAsync(bufs->status, 0, sizeof(uint32_t), s));
+  return set_error(MHPPO_ENAN, "NaN policy output sampled (%s%s%s): the reference raises ValueError here",
+                   (st & 1u) ? "Categorical probs of the choice actor, :409" : "", (st & 3u) == 3u ? "; " : "",
+                   (st & 2u) ? "MultivariateNormal loc of the continuous actors, :451" : "");
 }
 
 int mhppo_eval_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,

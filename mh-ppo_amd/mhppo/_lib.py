@@ -36,7 +36,7 @@ class RolloutBufs(ctypes.Structure):
     _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
                 ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
                 ("rew", P), ("ep_min", P), ("exist", P), ("rows", P), ("T", I32),
-                ("flags", I32)]
+                ("flags", I32), ("status", P)]
 
 
 class EvalBufs(ctypes.Structure):
@@ -68,6 +68,7 @@ _SIGS = {
     "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
     "mhppo_eval_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), I32,
                               ctypes.POINTER(EvalBufs), P]),
+    "mhppo_rollout_check": (I32, [ctypes.POINTER(RolloutBufs), P]),
     "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_normal_2d": (I32, [U64, U64, U64, P, I64, I64, P]),
@@ -88,6 +89,12 @@ _lib = None
 
 class MhppoError(RuntimeError):
     pass
+
+
+class MhppoNaNError(MhppoError, ValueError):
+    """MHPPO_ENAN: a NaN policy output was sampled (the reference raises ValueError there)."""
+
+ENAN = -4
 
 
 def lib():
@@ -111,7 +118,8 @@ def declared_symbols():
 
 def check(rc):
     if rc != 0:
-        raise MhppoError(f"libmhppo error {rc}: {lib().mhppo_last_error().decode()}")
+        cls = MhppoNaNError if rc == ENAN else MhppoError
+        raise cls(f"libmhppo error {rc}: {lib().mhppo_last_error().decode()}")
     return rc
 
 

@@ -75,6 +75,7 @@ class Env_rollout:
                                           iteration=self.iteration, forced_choice=forced_choice, eps_tape=eps_tape)
         self.iteration += 1
         self.cross, self.wait, self.choice = bucket_segments(self.batch, fix_bucket=self.fix_bucket)
+        self.gpu.check()  # NaN policy outputs raise, as torch.distributions does in the reference
         return self.batch
 
     # reference-named views of the collected batch
@@ -133,6 +134,11 @@ class Algo_PPO:
             for net in self.nets():  # replicas start identical (rank 0's init)
                 for p in net.parameters():
                     dist.broadcast(p.data, src=0)
+        # every net's flat gradient in one contiguous buffer: one in-place all-reduce per
+        # joint epoch under data parallelism (mhppo.ppo.GradBucket)
+        self.grad_bucket = ppo.GradBucket([self.actor_net_cross, self.critic_net_cross, self.actor_net_wait,
+                                           self.critic_net_wait, self.actor_net_choice, self.critic_net_choice],
+                                          dev)
         # one fused Adam launch per net and step on the GPU (the reference's default Adam
         # semantics: lr, betas (0.9, 0.999), eps 1e-8, no weight decay)
         A = (lambda params, lr: torch.optim.Adam(params, lr, fused=True)) if dev.type == "cuda" else torch.optim.Adam
@@ -178,34 +184,43 @@ class Algo_PPO:
             setattr(self, k, v)
 
     def update(self):
-        """10 epochs of cross+wait, then 10 epochs of choice (:868-882) on the collected batch."""
+        """10 epochs of cross+wait, then 10 epochs of choice (:868-882) on the collected batch,
+        run as 10 joint epochs of the three independent heads (mhppo.ppo.train_epoch: same
+        results, two collectives per epoch under data parallelism).  The global row counts
+        and choice action counts take one all-reduce and one host sync per iteration."""
         r = self.rollout
         dev = self.venv.device
         c, w, d = r.cross, r.wait, r.choice
-        m_c = ppo.global_count(c["ret"].numel(), dev)
-        m_w = ppo.global_count(w["ret"].numel(), dev)
-        m_d = ppo.global_count(d["ret"].numel(), dev)
-        counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
-        ppo._allreduce_(counts)
-        losses = {}
-        for _ in range(10):
-            if m_c > 0:
-                losses["cross"] = ppo.train_model_c(self.actor_net_cross, self.critic_net_cross,
-                                                    self.optimizer_actor_cross, self.optimizer_critic_cross,
-                                                    c["obs"], c["act"], c["logp"], c["ret"], m_c)
+        with torch.cuda.device(dev):
+            loc = torch.cat([torch.tensor([c["ret"].numel(), w["ret"].numel(), d["ret"].numel()],
+                                          dtype=torch.float64, device=dev),
+                             torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)])
+            ppo._allreduce_(loc)
+            m_c, m_w, m_d = loc[:3].tolist()
+            counts = loc[3:5]
+            heads, names = [], []
+            if m_c > 0:  # the reference trains a continuous head only on a non-empty batch (:869, :874)
+                heads.append(ppo.Head("c", self.actor_net_cross, self.critic_net_cross, self.optimizer_actor_cross,
+                                      self.optimizer_critic_cross, c["obs"], c["act"], c["logp"], c["ret"], m_c))
+                names.append("cross")
             if m_w > 0:
-                losses["wait"] = ppo.train_model_c(self.actor_net_wait, self.critic_net_wait,
-                                                   self.optimizer_actor_wait, self.optimizer_critic_wait,
-                                                   w["obs"], w["act"], w["logp"], w["ret"], m_w)
-        for _ in range(10):
-            if m_d > 0:
-                losses["choice"] = ppo.train_model_d(self.actor_net_choice, self.critic_net_choice,
-                                                     self.optimizer_actor_choice, self.optimizer_critic_choice,
-                                                     d["obs"], d["act"], d["logp"], d["ret"], m_d, counts,
-                                                     per_row=self.fix_choice_loss)
-        self.last_losses = {k: (float(a.item()) / (m_d * m_d if k == "choice" else (m_c if k == "cross" else m_w)),
-                                float(b.item()) / (m_d if k == "choice" else (m_c if k == "cross" else m_w)))
-                            for k, (a, b) in losses.items()} if self.verbose else losses
+                heads.append(ppo.Head("c", self.actor_net_wait, self.critic_net_wait, self.optimizer_actor_wait,
+                                      self.optimizer_critic_wait, w["obs"], w["act"], w["logp"], w["ret"], m_w))
+                names.append("wait")
+            if m_d > 0:  # never empty in the reference (>= 1 existing car per episode); it would raise there
+                heads.append(ppo.Head("d", self.actor_net_choice, self.critic_net_choice, self.optimizer_actor_choice,
+                                      self.optimizer_critic_choice, d["obs"], d["act"], d["logp"], d["ret"], m_d,
+                                      counts, per_row=self.fix_choice_loss))
+                names.append("choice")
+            losses = None
+            for _ in range(10):
+                losses = ppo.train_epoch(heads, self.grad_bucket)
+        if self.verbose and losses is not None:
+            div = {"cross": (m_c, m_c), "wait": (m_w, m_w), "choice": (m_d * m_d, m_d)}
+            if self.fix_choice_loss:
+                div["choice"] = (m_d, m_d)
+            self.last_losses = {k: (float(a.item()) / div[k][0], float(b.item()) / div[k][1])
+                                for k, (a, b) in zip(names, losses)}
         return m_c, m_w, m_d
 
     def evaluate(self, nbr_episodes, choix=False):
@@ -215,15 +230,26 @@ class Algo_PPO:
         return self.rollout.iterations(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
                                        nbr_episodes, choix=choix)
 
-    def train(self, nb_loop):
+    def get_average(self, states):
+        """The paper cell's evaluation statistics (get_average, :1550-1675; CO2 leg excluded)
+        over `states`, the observations evaluate() returned (mhppo.stats)."""
+        from .stats import get_average
+        v = self.venv
+        return get_average(states, v.variant, v.nb_car, v.nb_ped, v.nb_lines)
+
+    def train(self, nb_loop, replay=None):
         """(:854-917): per iteration rollout.reset() -> one episode per env -> 10 + 10 epochs
         -> reward curves -> rollout.reset() (both resets consume env draws, as in the
-        reference); at the end the curves go to load_model/parameters/*.npy (:908-916)."""
+        reference); at the end the curves go to load_model/parameters/*.npy (:908-916).
+        replay (parity tests): one (forced_choice, eps_tape) pair per iteration, the
+        recorded Categorical and MVN draws replayed instead of Philox noise."""
         self.rollout.fix_bucket = self.fix_bucket
         for ep in range(nb_loop):
             self.rollout.reset()
+            fc, et = replay[ep] if replay is not None else (None, None)
             self.rollout.iterations_rand(self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
-                                         self.cov_mat, self.cov_mat_d, self.batch_size)
+                                         self.cov_mat, self.cov_mat_d, self.batch_size, forced_choice=fc,
+                                         eps_tape=et)
             m_c, m_w, m_d = self.update()
             rc, rw, rd = self.rollout.immediate_rewards()
             dev = self.venv.device
@@ -234,7 +260,7 @@ class Algo_PPO:
                 self.ep_reward_cross.append(sums[0] / m_c)
             if m_w > 0:
                 self.ep_reward_wait.append(sums[1] / m_w)
-            self.ep_reward_choice.append(sums[2] / max(m_d, 1))
+            self.ep_reward_choice.append(sums[2] / m_d if m_d > 0 else float("nan"))  # mean() of empty: NaN
             self.ep_scenario_balance.append([int(m_c), int(m_w)])
             if self.verbose and _rank() == 0:
                 print("Episode * {} * And Number of steps is ==> {}".format(ep, ep * self.batch_size))

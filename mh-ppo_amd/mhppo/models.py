@@ -49,7 +49,11 @@ class Model_PPO(nn.Module):
     def _flatten(self):
         ps = self._params()
         flat = torch.cat([p.detach().reshape(-1) for p in ps]).float().contiguous()
-        gflat = torch.zeros_like(flat)
+        gb = getattr(self, "_gbound", None)  # storage given by bind_grad (a GradBucket slice)
+        if gb is not None and gb.numel() == flat.numel() and gb.device == flat.device:
+            gflat = gb
+        else:
+            gflat = torch.zeros_like(flat)
         off = 0
         with torch.no_grad():
             for p in ps:
@@ -89,6 +93,21 @@ class Model_PPO(nn.Module):
                 p.grad = self._gflat[off:off + n].view_as(p)
             off += n
         return self._gflat
+
+    def bind_grad(self, storage):
+        """Make `storage` (float32, one element per parameter, on the net's device) the flat
+        gradient the parameters' .grad views alias (mhppo.ppo.GradBucket)."""
+        if storage.numel() != self.flat().numel() or storage.dtype != torch.float32:
+            raise ValueError("gradient storage must be float32 with one element per parameter")
+        self._gbound = storage
+        self._gflat = storage
+        off = 0
+        with torch.no_grad():
+            for p in self._params():
+                n = p.numel()
+                p.grad = storage[off:off + n].view_as(p)
+                off += n
+        return self
 
     def forward(self, input1):
         if isinstance(input1, np.ndarray):

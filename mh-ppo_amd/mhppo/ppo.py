@@ -1,21 +1,28 @@
 """PPO update of the multi-head actor-critic (Algo_PPO.train_model_c / _d,
 Coop-MH-PPO-scalable.py:778-851), full batch, on the GPU.
 
-The MLP forward/backward stays in PyTorch-ROCm (tiny GEMMs + autograd); the
-PPO arithmetic around it is hand-written HIP (include/mhppo.h):
-  advantage stats + normalisation  (A - mean) / (std_unbiased + 1e-10)   :786-787
-  continuous clip surrogate, float64 ratio, dL/dmu                        :795-806
-  choice surrogate over the M x M broadcast, exact O(M) form, dL/dprobs   :834-842
-  critic MSE and dL/dV                                                    :808-809
-Epoch semantics follow the reference: the advantage uses the critic of the
-start of the epoch, the actor-loss gradient never reaches the critic (the
-reference zeroes it before the critic step, :810-815), Adam for each net.
+Every head's epoch runs on the fused f32-MFMA training kernel (mhppo_mlp_train,
+csrc/mlp_train.hip): a critic pass (forward, MSE gradient, advantage sums) and an
+actor pass (forward, clip-surrogate gradient against the advantage normalised with
+the start-of-epoch critic, backward, weight gradients); Adam (fused) steps each net.
+Epoch semantics follow the reference: the advantage uses the critic of the start of
+the epoch (:784-787), the actor-loss gradient never reaches the critic (the reference
+zeroes it before the critic step, :810-815).  The small HIP kernels below (advantage
+statistics, the clip surrogates, MSE) restate the same losses for the tests'
+autograd cross-checks.
 
-Data parallel: every rank holds a shard of the batch; advantage sums and the
-choice action counts are all-reduced (SUM) so normalisation uses the global
-batch, each rank's gradient is the gradient of (global-mean loss restricted to
-its rows), and one flat all-reduce (SUM) per update makes it the full-batch
-gradient.  Adam then runs replicated.
+Heads are independent nets, so one epoch of every head of an iteration runs together
+(train_epoch): the reference's 10 cross/wait epochs and its 10 choice epochs
+(:868-882) become 10 joint epochs with identical results.
+
+Data parallel: every rank holds a shard of every head's batch.  Per
+joint epoch there are exactly two collectives: one all-reduce (SUM, float64) of all
+heads' advantage sums between the critic and the actor passes, and one all-reduce
+(SUM) of the gradient bucket — every net's flat gradient lives in one contiguous
+GradBucket, so the collective runs in place with no pack/unpack copies.  Each rank's
+gradient is that of (global-mean loss restricted to its rows), so the reduced
+gradient is the full-batch gradient; Adam then runs replicated.  A rank whose shard
+of a head is empty still joins both collectives (the kernel writes a zero gradient).
 """
 import torch
 import torch.distributed as dist
@@ -33,38 +40,53 @@ def _allreduce_(t):
     return t
 
 
-def _allreduce_net_grads(*nets):
-    """One all-reduce (SUM) of the nets' flat gradients (the .grad views alias them)."""
-    if not _dp():
-        return
-    if all(hasattr(n, "grad_flat") for n in nets):
-        flats = [n.grad_flat() for n in nets]
-        flat = torch.cat(flats)
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-        off = 0
-        for f in flats:
-            f.copy_(flat[off:off + f.numel()])
-            off += f.numel()
-        return
-    _allreduce_grads([p for n in nets for p in n.parameters()])
-
-
-def _allreduce_grads(params):
-    if not _dp():
-        return
-    grads = [p.grad for p in params]
-    flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-    off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
-        off += n
+def global_counts(values, device):
+    """All-reduce (SUM) a few per-rank counts at once; one host sync: returns floats."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    return [float(x) for x in _allreduce_(t).tolist()]
 
 
 def global_count(n, device):
-    t = torch.tensor([float(n)], dtype=torch.float64, device=device)
-    return float(_allreduce_(t).item())
+    return global_counts([n], device)[0]
+
+
+class GradBucket:
+    """One contiguous float32 buffer holding the flat gradients of several Model_PPOs
+    (each net's .grad views alias its slice): the gradient all-reduce of an epoch is
+    one in-place collective over a contiguous span of it."""
+
+    def __init__(self, nets, device):
+        sizes = [n.flat().numel() for n in nets]
+        self.buf = torch.zeros(sum(sizes), dtype=torch.float32, device=device)
+        self.span = {}
+        off = 0
+        for net, n in zip(nets, sizes):
+            net.bind_grad(self.buf[off:off + n])
+            self.span[id(net)] = (off, off + n)
+            off += n
+
+    def allreduce(self, nets):
+        """In-place SUM over the smallest contiguous span covering `nets`' gradients."""
+        if not _dp() or not nets:
+            return
+        for n in nets:  # re-link any .grad that autograd / zero_grad rebound
+            n.grad_flat()
+        lo = min(self.span[id(n)][0] for n in nets)
+        hi = max(self.span[id(n)][1] for n in nets)
+        dist.all_reduce(self.buf[lo:hi], op=dist.ReduceOp.SUM)
+
+
+def _allreduce_net_grads(*nets):
+    """Gradient all-reduce for nets outside a GradBucket (one packed collective)."""
+    if not _dp():
+        return
+    flats = [n.grad_flat() for n in nets]
+    flat = torch.cat(flats)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    off = 0
+    for f in flats:
+        f.copy_(flat[off:off + f.numel()])
+        off += f.numel()
 
 
 # ---------------------------------------------------------------- kernel layer
@@ -77,7 +99,7 @@ def k_adv_stats(ret, value):
     v = value.detach().contiguous()
     with torch.cuda.device(ret.device):
         _lib.check(_lib.lib().mhppo_adv_stats(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
-                                          _lib.stream_ptr()))
+                                              _lib.stream_ptr()))
     return stats
 
 
@@ -86,7 +108,7 @@ def k_adv_normalize(ret, value, stats, m_global):
     v = value.detach().contiguous()
     with torch.cuda.device(ret.device):
         _lib.check(_lib.lib().mhppo_adv_normalize(_lib.ptr(ret), _lib.ptr(v), ret.numel(), _lib.ptr(stats),
-                                              float(m_global), _lib.ptr(adv), _lib.stream_ptr()))
+                                                  float(m_global), _lib.ptr(adv), _lib.stream_ptr()))
     return adv
 
 
@@ -95,8 +117,8 @@ def k_mse(value, ret, m_global):
     loss = torch.zeros(1, dtype=torch.float64, device=ret.device)
     v = value.detach().contiguous()
     with torch.cuda.device(ret.device):
-        _lib.check(_lib.lib().mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global, _lib.ptr(dv),
-                                            _lib.ptr(loss), _lib.stream_ptr()))
+        _lib.check(_lib.lib().mhppo_mse_fwd_bwd(_lib.ptr(v), _lib.ptr(ret), ret.numel(), 1.0 / m_global,
+                                                _lib.ptr(dv), _lib.ptr(loss), _lib.stream_ptr()))
     return dv, loss
 
 
@@ -106,8 +128,8 @@ def k_ppo_cont(mu, act, logp_old, adv, m_global):
     m = mu.detach().contiguous()
     with torch.cuda.device(adv.device):
         _lib.check(_lib.lib().mhppo_ppo_cont_fwd_bwd(_lib.ptr(m), _lib.ptr(act), _lib.ptr(logp_old), _lib.ptr(adv),
-                                                 adv.numel(), 1.0 / m_global, _lib.ptr(dmu), _lib.ptr(loss),
-                                                 _lib.stream_ptr()))
+                                                     adv.numel(), 1.0 / m_global, _lib.ptr(dmu), _lib.ptr(loss),
+                                                     _lib.stream_ptr()))
     return dmu, loss
 
 
@@ -117,8 +139,8 @@ def k_ppo_choice(probs, logp_old, adv, counts, m_global):
     loss = torch.zeros(1, dtype=torch.float64, device=adv.device)
     with torch.cuda.device(adv.device):
         _lib.check(_lib.lib().mhppo_ppo_choice_fwd_bwd(_lib.ptr(p), _lib.ptr(logp_old), _lib.ptr(adv), adv.numel(),
-                                                   _lib.ptr(counts), 1.0 / (m_global * m_global), _lib.ptr(dp),
-                                                   _lib.ptr(loss), _lib.stream_ptr()))
+                                                       _lib.ptr(counts), 1.0 / (m_global * m_global), _lib.ptr(dp),
+                                                       _lib.ptr(loss), _lib.stream_ptr()))
     return dp, loss
 
 
@@ -136,6 +158,7 @@ def flops_per_row(n_in, n_out):
 
 
 FLOPS_PER_ROW_CONT = flops_per_row(13, 1)
+N_IN_MAX = 64  # the fused kernel's widest input (scalable 8-slot choice head: dc = 54)
 
 KIND_CRITIC, KIND_CONT, KIND_CHOICE = 0, 1, 2
 
@@ -148,9 +171,10 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     """Fused forward/loss/backward of one head (mhppo_mlp_train).
     kind 0 (critic): returns (grad, sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
     kind 1 (continuous actor) / 2 (choice actor): returns (grad, sums[3] = (sum surrogate, 0, 0), None).
-    grad is the packed torch-layout gradient (W1 b1 .. W4 b4)."""
+    grad is the packed torch-layout gradient (W1 b1 .. W4 b4), written into the net's flat
+    .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient."""
     want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
-    if net.model_type != want or net.n_in > 32 or (kind == KIND_CONT and net.n_in != 13):
+    if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):
         raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
                          f"{net.n_in}->{net.n_out} Model_PPO")
     dev = obs.device
@@ -163,12 +187,11 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     act = None if act is None else act.float().contiguous()
     logp_old = None if logp_old is None else logp_old.float().contiguous()
     np_ = n_params(net.n_in, net.n_out)
-    # the gradient lands straight in the net's flat .grad storage when it has one
-    grad = net.grad_flat() if hasattr(net, "grad_flat") else None
-    if grad is None or grad.numel() != np_ or grad.device != dev:
-        grad = torch.empty(np_, dtype=torch.float32, device=dev)
+    grad = net.grad_flat()
+    if grad.numel() != np_ or grad.device != dev:
+        raise ValueError("gradient storage does not match the net / the batch's device")
     sums = torch.zeros(3, dtype=torch.float64, device=dev)
-    w = net.flat() if hasattr(net, "flat") else net.packed()
+    w = net.flat()
     p = _lib.ptr
     ev = None
     if TRAIN_EVENTS is not None:
@@ -186,106 +209,59 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
 
 # ------------------------------------------------------------- DP orchestration
 
-def normalized_advantage(ret, value, m_global):
-    stats = _allreduce_(k_adv_stats(ret, value))
-    return k_adv_normalize(ret, value, stats, m_global)
+class Head:
+    """One actor/critic pair, its Adam optimisers and this rank's shard of its batch.
+    kind "c": continuous head (train_model_c, :778-815); "d": choice head (train_model_d,
+    :818-851) with the GLOBAL action counts (n0, n1) of the M x M broadcast, or the
+    opt-in per-row loss.  m = the global row count."""
+
+    def __init__(self, kind, actor, critic, opt_actor, opt_critic, obs, act, logp, ret, m, counts=None,
+                 per_row=False):
+        self.kind, self.actor, self.critic = kind, actor, critic
+        self.opt_actor, self.opt_critic = opt_actor, opt_critic
+        self.obs, self.act, self.logp, self.ret, self.m = obs, act, logp, ret, float(m)
+        self.counts = None if counts is None else counts.double().contiguous()
+        self.per_row = per_row
 
 
-def _set_grads(net, flat):
-    if hasattr(net, "_gflat") and flat is net._gflat:
-        return  # written in place (k_mlp_train)
-    off = 0
-    for lay in (net.layer1, net.layer2, net.layer3, net.layer4):
-        for p in (lay.weight, lay.bias):
-            n = p.numel()
-            g = flat[off:off + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            off += n
+def train_epoch(heads, bucket=None):
+    """One full-batch epoch of every head: critic passes -> ONE all-reduce of all heads'
+    advantage sums -> actor passes -> ONE gradient all-reduce -> Adam.  Returns this rank's
+    (actor, critic) loss sums per head (float64 [1] tensors)."""
+    crit = [k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m) for h in heads]
+    stats = torch.cat([sc[1:3] for _, sc, _ in crit])
+    _allreduce_(stats)
+    out = []
+    for i, (h, (_, sc, V)) in enumerate(zip(heads, crit)):
+        st = stats[2 * i:2 * i + 2]
+        if h.kind == "c":
+            _, sa, _ = k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m)
+        elif h.per_row:
+            _, sa, _ = k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, h.act.float(), h.logp, st, None,
+                                   m_global=h.m)
+        else:
+            _, sa, _ = k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, None, h.logp, st, h.counts, m_global=h.m)
+        out.append((sa[0:1], sc[0:1]))
+    nets = [n for h in heads for n in (h.actor, h.critic)]
+    if bucket is not None:
+        bucket.allreduce(nets)
+    else:
+        _allreduce_net_grads(*nets)
+    for h in heads:
+        h.opt_actor.step()
+        h.opt_critic.step()
+    return out
 
 
 def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
-    """One full-batch epoch of Algo_PPO.train_model_c (:778-815) on the fused MFMA kernel:
-    critic pass (V, MSE gradient, advantage sums) -> all-reduce of the sums -> actor pass
-    (clip-surrogate gradient w.r.t. the start-of-epoch critic's advantage) -> one gradient
-    all-reduce -> Adam.  Returns this rank's (actor, critic) loss sums (float64 tensors)."""
-    gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
-    stats = _allreduce_(sc[1:3].clone())
-    ga, sa, _ = k_mlp_train(KIND_CONT, actor, obs, ret, V, act, logp_old, stats, m_global=m_global)
-    _set_grads(critic, gc)
-    _set_grads(actor, ga)
-    _allreduce_net_grads(actor, critic)
-    opt_actor.step()
-    opt_critic.step()
-    return sa[0:1], sc[0:1]
-
-
-def train_model_c_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
-    """train_model_c with the MLPs in PyTorch autograd and the PPO arithmetic in HIP
-    (kept as the cross-check for the fused kernel)."""
-    V = torch.squeeze(critic(obs), -1)
-    adv = normalized_advantage(ret, V, m_global)
-    mu = torch.squeeze(actor(obs), -1)
-    dmu, la = k_ppo_cont(mu, act, logp_old, adv, m_global)
-    dv, lc = k_mse(V, ret, m_global)
-    opt_actor.zero_grad(set_to_none=False)
-    opt_critic.zero_grad(set_to_none=False)
-    torch.autograd.backward([mu, V], [dmu, dv])
-    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
-    opt_actor.step()
-    opt_critic.step()
-    return la, lc  # this rank's loss sums (logging only; reduce if needed)
+    """One full-batch epoch of Algo_PPO.train_model_c (:778-815) for one head.
+    Returns this rank's (actor, critic) loss sums (float64 tensors)."""
+    return train_epoch([Head("c", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global)])[0]
 
 
 def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row=False):
-    """One full-batch epoch of Algo_PPO.train_model_d (:818-851) on the fused kernel:
-    critic pass -> all-reduce of the advantage sums -> choice-actor pass (O(M) form of the
-    M x M Categorical surrogate with the global action counts) -> gradient all-reduce ->
-    Adam.  counts = global (n0, n1) float64.  per_row=True is the opt-in bug fix (SURVEY
-    §8(f)4): the standard per-row PPO surrogate (each row's own action, mean over rows)
-    instead of the reference's M x M broadcast.  Returns this rank's (actor, critic) loss sums."""
-    if per_row:
-        if critic.n_in > 32:
-            raise ValueError("per-row choice loss needs the fused kernel (n_in <= 32)")
-        gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
-        stats = _allreduce_(sc[1:3].clone())
-        ga, sa, _ = k_mlp_train(KIND_CHOICE, actor, obs, ret, V, act.float(), logp_old, stats, None,
-                                m_global=m_global)
-        _set_grads(critic, gc)
-        _set_grads(actor, ga)
-        _allreduce_net_grads(actor, critic)
-        opt_actor.step()
-        opt_critic.step()
-        return sa[0:1], sc[0:1]
-    if critic.n_in > 32:
-        return train_model_d_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global,
-                                      counts)
-    gc, sc, V = k_mlp_train(KIND_CRITIC, critic, obs, ret, m_global=m_global)
-    stats = _allreduce_(sc[1:3].clone())
-    ga, sa, _ = k_mlp_train(KIND_CHOICE, actor, obs, ret, V, None, logp_old, stats, counts.double().contiguous(),
-                            m_global=m_global)
-    _set_grads(critic, gc)
-    _set_grads(actor, ga)
-    _allreduce_net_grads(actor, critic)
-    opt_actor.step()
-    opt_critic.step()
-    return sa[0:1], sc[0:1]
-
-
-def train_model_d_autograd(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts):
-    """train_model_d with the MLPs in PyTorch autograd and the PPO arithmetic in HIP (choice
-    observations wider than the fused kernel's 32 inputs; cross-check for the fused kernel)."""
-    V = torch.squeeze(critic(obs), -1)
-    adv = normalized_advantage(ret, V, m_global)
-    probs = actor(obs).reshape(-1, 2)
-    dp, la = k_ppo_choice(probs, logp_old, adv, counts, m_global)
-    dv, lc = k_mse(V, ret, m_global)
-    opt_actor.zero_grad(set_to_none=False)
-    opt_critic.zero_grad(set_to_none=False)
-    torch.autograd.backward([probs, V], [dp, dv])
-    _allreduce_grads(list(actor.parameters()) + list(critic.parameters()))
-    opt_actor.step()
-    opt_critic.step()
-    return la, lc  # this rank's loss sums (logging only; reduce if needed)
+    """One full-batch epoch of Algo_PPO.train_model_d (:818-851) for one head: O(M) form of
+    the M x M Categorical surrogate with the global action counts (n0, n1); per_row=True is
+    the opt-in bug fix.  Returns this rank's (actor, critic) loss sums."""
+    h = Head("d", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row)
+    return train_epoch([h])[0]

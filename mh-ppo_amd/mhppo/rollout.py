@@ -63,9 +63,10 @@ class RolloutGPU:
         self.eps = z((self.T, N, S), f32)
         self.u = z((N, S, P), f32)
         self.rows = z(N * S * P + 2, i32)  # head-sorted policy rows (filled by mhppo_rollout_begin)
+        self.status = z(1, i32)  # NaN flags of the policy draws (mhppo_rollout_check)
         b = _lib.RolloutBufs()
         for name in ("feat_d", "probs_d", "logp_d", "a_d", "closest", "feat_c", "out_c", "obs", "obs_c", "act",
-                     "logp", "rew", "ep_min", "exist", "rows"):
+                     "logp", "rew", "ep_min", "exist", "rows", "status"):
             setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
         b.T = self.T
         # policy step on the VALU kernel instead of the MFMA one (bit-identical; A/B and tests)
@@ -111,6 +112,11 @@ class RolloutGPU:
         saved = cat["saved"].reshape(-1).bool()
         return (cat["obs"].reshape(-1, venv.obs_dim), cat["acts"].reshape(-1, S), cat["rews_c"].reshape(-1, S),
                 cat["rews_d"].reshape(-1, S)[saved], cat["waiting"].reshape(-1, P)[saved].reshape(-1))
+
+    def check(self):
+        """Raise MhppoNaNError (a ValueError, as the reference's torch.distributions raise) if
+        a NaN policy output was sampled since the last check.  Synchronises the stream."""
+        _lib.check(_lib.lib().mhppo_rollout_check(ctypes.byref(self._bufs), _lib.stream_ptr(device=self.venv.device)))
 
     def draw_noise(self, seed, iteration):
         """Philox perf-mode noise for one iteration (global-env-id counters)."""

@@ -49,20 +49,39 @@ def _install_cpu_doubles(ppo):
         dmu = (1.0 / m) * (-g) * r * x.double() / L
         return dmu.float(), (-torch.minimum(s1, s2)).sum().reshape(1)
 
+    def choice_loss(probs, lp_old, adv, counts, m):
+        """O(M) form of the M x M Categorical surrogate (include/mhppo.h), float64, differentiable."""
+        p = probs.double().reshape(-1, 2)
+        pn = p / p.sum(1, keepdim=True)
+        eps = 1.1920928955078125e-07
+        pc = pn.clamp(eps, 1 - eps)
+        r = torch.exp(torch.log(pc) - lp_old.double().reshape(-1, 1))
+        A = adv.double().reshape(-1, 1)
+        f = -torch.minimum(r * A, r.clamp(0.8, 1.2) * A)
+        return (f * counts.reshape(1, 2)).sum()
+
     def mlp_train(kind, net, obs, ret, value=None, act=None, lp_old=None, stats=None, counts=None, m_global=1.0):
         m = m_global
         params = list(net.parameters())
         out = torch.squeeze(net(obs), -1)
+        gf = net.grad_flat()  # the kernel writes the gradient into the net's flat storage
         if kind == 0:
             dv, loss = mse(out, ret, m)
             st = adv_stats(ret, out)
             sums = torch.cat([loss, st])
-            g = torch.autograd.grad(out, params, dv)
-            return torch.cat([x.reshape(-1) for x in g]), sums, out.detach()
+            g = torch.autograd.grad(out, params, dv, allow_unused=True)
+            gf.copy_(torch.cat([(x if x is not None else torch.zeros_like(q)).reshape(-1) for x, q in zip(g, params)]))
+            return gf, sums, out.detach()
         adv = adv_normalize(ret, value, stats, m)
-        dmu, loss = ppo_cont(out, act, lp_old, adv, m)
-        g = torch.autograd.grad(out, params, dmu)
-        return torch.cat([x.reshape(-1) for x in g]), torch.cat([loss, torch.zeros(2, dtype=torch.float64)]), None
+        if kind == 2:
+            loss = choice_loss(out, lp_old, adv, counts, m)
+            g = torch.autograd.grad(loss / (m * m), params, allow_unused=True)
+            loss = loss.detach().reshape(1)
+        else:
+            dmu, loss = ppo_cont(out, act, lp_old, adv, m)
+            g = torch.autograd.grad(out, params, dmu, allow_unused=True)
+        gf.copy_(torch.cat([(x if x is not None else torch.zeros_like(q)).reshape(-1) for x, q in zip(g, params)]))
+        return gf, torch.cat([loss, torch.zeros(2, dtype=torch.float64)]), None
 
     ppo.k_adv_stats, ppo.k_adv_normalize, ppo.k_mse, ppo.k_ppo_cont = adv_stats, adv_normalize, mse, ppo_cont
     ppo.k_mlp_train = mlp_train
@@ -112,5 +131,68 @@ def test_dp2_equals_single_process():
             rng.normal(-0.6, 0.3, M).astype(np.float32), rng.normal(-20, 8, M).astype(np.float32))
     single = _spawn(1, data)
     dp2 = _spawn(2, data)
+    for a, b in zip(single, dp2):
+        np.testing.assert_allclose(a, b, rtol=0, atol=2e-6)
+
+
+def _run_joint(rank, world, port, data, shards, out_q):
+    """Three heads (cross, wait, choice) trained by ppo.train_epoch with a GradBucket: two
+    collectives per joint epoch.  `shards[rank]` gives this rank's [lo, hi) rows per head
+    (an empty range = an empty shard that must still join every collective)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
+    from mhppo import ppo
+    from mhppo.models import Model_PPO
+    _install_cpu_doubles(ppo)
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    nets = [Model_PPO(13, 1, 1, mean=-1.0, std=3.0), Model_PPO(13, 1, 0), Model_PPO(13, 1, 1, mean=-1.0, std=3.0),
+            Model_PPO(13, 1, 0), Model_PPO(20, 2, 2), Model_PPO(20, 1, 0)]
+    bucket = ppo.GradBucket(nets, "cpu")
+    opts = [torch.optim.Adam(n.parameters(), 3e-4 if i % 2 == 0 else 1e-3) for i, n in enumerate(nets)]
+    heads = []
+    for h, kind in enumerate(("c", "c", "d")):
+        obs, act, lp, ret = (torch.tensor(x) for x in data[h])
+        lo, hi = shards[rank][h]
+        m = ppo.global_count(hi - lo, "cpu")
+        counts = None
+        if kind == "d":
+            counts = ppo._allreduce_(torch.stack([(act[lo:hi] == 0).sum(), (act[lo:hi] == 1).sum()]).double())
+        heads.append(ppo.Head(kind, nets[2 * h], nets[2 * h + 1], opts[2 * h], opts[2 * h + 1], obs[lo:hi],
+                              act[lo:hi], lp[lo:hi], ret[lo:hi], m, counts))
+    for _ in range(3):
+        ppo.train_epoch(heads, bucket)
+    if rank == 0:
+        out_q.put([p.detach().numpy().copy() for n in nets for p in n.parameters()])
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _spawn_joint(world, data, shards):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30600 + os.getpid() % 1000 + world
+    procs = [ctx.Process(target=_run_joint, args=(r, world, port, data, shards, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_dp2_joint_epoch_with_empty_shard():
+    """The joint three-head epoch (one advantage-sum and one gradient-bucket all-reduce per
+    epoch) over 2 ranks equals one process; rank 1 holds NO wait rows and still joins."""
+    rng = np.random.default_rng(3)
+    data = []
+    for M, nin, choice in ((500, 13, False), (120, 13, False), (90, 20, True)):
+        act = ((rng.uniform(size=M) < 0.4).astype(np.float32) if choice else rng.normal(-1, 1, M).astype(np.float32))
+        data.append((rng.normal(0, 3, (M, nin)).astype(np.float32), act, rng.normal(-0.6, 0.3, M).astype(np.float32),
+                     rng.normal(-20, 8, M).astype(np.float32)))
+    single = _spawn_joint(1, data, [[(0, 500), (0, 120), (0, 90)]])
+    dp2 = _spawn_joint(2, data, [[(0, 230), (0, 120), (0, 40)], [(230, 500), (120, 120), (40, 90)]])
     for a, b in zip(single, dp2):
         np.testing.assert_allclose(a, b, rtol=0, atol=2e-6)

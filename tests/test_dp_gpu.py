@@ -26,3 +26,27 @@ def test_two_ranks_equal_one_process(tmp_path):
     assert a.shape == b.shape
     assert np.isfinite(a).all()
     np.testing.assert_allclose(b, a, rtol=0, atol=1e-5)
+
+
+def test_bench_launches_two_ranks(tmp_path):
+    """`bench.py --gpus 2` starts its own two ranks (torch.distributed.run, gloo rehearsal on
+    the box's one GPU), reports n_gpus 2 and the world's env ranges, and its two ranks of
+    1024 envs train the same nets as one rank of 2048 envs (global-id env streams and noise)."""
+    import json
+    one, two = str(tmp_path / "one.npy"), str(tmp_path / "two.npy")
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    common = ["--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dist-backend", "gloo"]
+    out1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--envs", "2048",
+                           "--save-nets", one] + common, check=True, timeout=300, env=env, cwd=tmp_path,
+                          capture_output=True, text=True).stdout
+    out2 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--envs", "1024",
+                           "--save-nets", two] + common, check=True, timeout=300, env=env, cwd=tmp_path,
+                          capture_output=True, text=True).stdout
+    l1 = json.loads([x for x in out1.splitlines() if x.startswith("{")][-1])
+    l2 = json.loads([x for x in out2.splitlines() if x.startswith("{")][-1])
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    assert l2["dist"]["world_size"] == 2 and l2["dist"]["env_ranges"] == [[0, 1024], [1024, 2048]]
+    a, b = np.load(one), np.load(two)
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(b, a, rtol=0, atol=1e-5)

@@ -54,6 +54,7 @@ def test_fullscale_discrete_parity(case):
     div = np.zeros(N, bool)          # any discrete mismatch so far
     first_div = np.full(N, -1)
     n_bits = n_tot = 0
+    r_bits = r_tot = 0  # rewards + reward_light only
     max_rel = max_rel_obs = 0.0
     for t in range(T):
         acc = rng.uniform(-4.5, 2.5, size=(N, S)).astype(np.float32).astype(np.float64)
@@ -73,9 +74,13 @@ def test_fullscale_discrete_parity(case):
         ok = ~div
         for g, ref in ((r, ro), (rl, rlo), (st, dm), (o, oo)):
             is_obs = g is o
+            is_rew = g is r or g is rl
             g, ref = g[ok].astype(np.float64), ref[ok].astype(np.float64)
             n_bits += int((g != ref).sum())
             n_tot += g.size
+            if is_rew:
+                r_bits += int((g != ref).sum())
+                r_tot += g.size
             if g.size:
                 rel = float(np.nanmax(np.abs(g - ref) / np.maximum(np.abs(ref), 1e-3)))
                 if is_obs:
@@ -89,6 +94,7 @@ def test_fullscale_discrete_parity(case):
                mt_state_mismatch_envs=int(mt_bad.sum()), first_divergence_steps=sorted(set(first_div[div].tolist()))[:20],
                diverged_env_ids=np.nonzero(div)[0][:20].tolist(), float_outputs_bit_different=n_bits,
                float_outputs=n_tot, bit_different_fraction=n_bits / max(n_tot, 1),
+               reward_bit_different_fraction=r_bits / max(r_tot, 1),
                max_rel_err_f64_undiverged=max_rel, max_rel_err_obs_f32_undiverged=max_rel_obs)
     _report(v, rec)
     assert rec["diverged_envs"] == 0 and rec["mt_state_mismatch_envs"] == 0, rec

@@ -108,3 +108,32 @@ def test_choix_rejected_off_scalable():
     from mhppo._lib import MhppoError
     with pytest.raises(MhppoError):
         algo.evaluate(1, choix=True)
+
+
+STATS = sorted(f[6:-4] for f in os.listdir(os.path.join(ROOT, "tests", "golden")) if f.startswith("stats_"))
+
+
+@pytest.mark.parametrize("name", STATS)
+def test_gpu_get_average_matches_reference(name):
+    """get_average (:1550-1675) over the GPU's own evaluation (computed on the device) vs the
+    reference function on the reference's trajectories (tests/golden/stats_*.npz): shares
+    exact, statistics within float32 noise of the trajectories."""
+    import oracle
+    from mhppo.env import VecCrosswalk
+    from mhppo.stats import get_average
+    from test_stats import _check
+    s = np.load(os.path.join(ROOT, "tests", "golden", f"stats_{name}.npz"))
+    g = np.load(os.path.join(ROOT, "tests", "golden", str(s["eval_fixture"])))
+    E, K, variant = len(g["n_obs"]), int(g["episodes"]), str(g["variant"])
+    venv = VecCrosswalk(variant, E, int(g["nb_car"]), int(g["nb_ped"]), int(g["nb_lines"]),
+                        seed_base=int(g["seed_base"]))
+    nets = _nets(g["w_cross"], g["w_wait"], g["w_choice"], oracle.choice_dim(variant, venv.n_slots))
+    from mhppo.rollout import RolloutGPU
+    venv.reset(want_obs=False)
+    states = RolloutGPU(venv).evaluate(*nets, K, choix="choix" in name)[0]
+    assert states.is_cuda
+    got = get_average(states, variant, venv.nb_car, venv.nb_ped, venv.nb_lines)
+    for k in ("yield_share", "go_share", "could_stop_share", "episodes"):
+        if k in s.files:
+            assert got[k] == float(s[k]) or (np.isnan(got[k]) and np.isnan(float(s[k]))), k
+    _check(got, s, 1e-4)

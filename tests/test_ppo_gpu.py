@@ -133,10 +133,12 @@ def test_fused_cont_grads_vs_autograd(M):
     _close_grad(ga, gat)
 
 
-@pytest.mark.parametrize("M,dc", [(1, 12), (45, 17), (4096, 27), (20001, 30), (333, 32)])
+@pytest.mark.parametrize("M,dc", [(1, 12), (45, 17), (4096, 27), (20001, 30), (333, 32), (70, 54), (65536, 54),
+                                  (1000, 40), (257, 64)])
 def test_fused_choice_grads_vs_autograd(M, dc):
-    """mhppo_mlp_train kinds 0/2 on choice-head shapes (dc = 12..32 inputs, 2-way softmax,
-    O(M) count-weighted surrogate) vs torch autograd + the HIP choice-loss kernel."""
+    """mhppo_mlp_train kinds 0/2 on choice-head shapes (dc = 12..64 inputs — 54 is the
+    scalable 8-slot driver's choice head, 2-way softmax, O(M) count-weighted surrogate) vs
+    torch autograd + the HIP choice-loss kernel."""
     from mhppo import ppo
     from mhppo.models import Model_PPO
     torch.manual_seed(M + dc)
