@@ -42,14 +42,20 @@ class _HostBackend:
         return self.h.state()
 
 
-def _train(env, nc, nl, npd):
+def _train(env, nc, nl, npd, driver="coop"):
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden", "gen"))
     import refclasses
-    ns = refclasses.notebook_classes("coop", env=env, nb_lines=nl, nb_car=nc, nb_ped=npd)
+    if driver == "coop":
+        ns = refclasses.notebook_classes("coop", env=env, nb_lines=nl, nb_car=nc, nb_ped=npd)
+        dc = 2 + 5 * (nc - 1) + 10
+    else:  # Coop-MH-PPO-scalable.py (:1036-1052)
+        ns = refclasses.scalable_classes(env=env, nb_lines=nl)
+        dc = 2 + 6 * (2 * nl - 1) + 10
     torch.manual_seed(0)
     with contextlib.redirect_stdout(io.StringIO()):
-        algo = ns["Algo_PPO"](ns["Model_PPO"], env, num_algo=122, num_states_c=13, num_states_d=2 + 5 * (nc - 1) + 10,
-                              num_actions=1, mean=-1.0, std=3.0, nb_cars=nc, dt=0.3, batch_size=160)
+        algo = ns["Algo_PPO"](ns["Model_PPO"], env, num_algo=100 * npd + 10 * nc + nl, num_states_c=13,
+                              num_states_d=dc, num_actions=1, mean=-1.0, std=3.0, nb_cars=nc, dt=0.3,
+                              batch_size=160)
         algo.train(1)
     ro = algo.rollout
     batch = [np.array(ro.batch_obs_cross + ro.batch_obs_wait), np.array(ro.batch_acts_cross + ro.batch_acts_wait),
@@ -78,6 +84,31 @@ def test_reference_driver_trains_on_facade_bit_identically(tmp_path, monkeypatch
     assert fac.observation_space["env"].shape == ref_env.observation_space["env"].shape
     assert fac.observation_space["ped"].shape == ref_env.observation_space["ped"].shape
     b_fac, w_fac = _train(fac, nc, nl, npd)
+    for x, y in zip(b_ref, b_fac):
+        assert np.array_equal(x, y)
+    for x, y in zip(w_ref, w_fac):
+        assert np.array_equal(x, y)
+
+
+def test_scalable_driver_trains_on_facade_bit_identically(tmp_path, monkeypatch):
+    """The same with Coop-MH-PPO-scalable.py's driver classes on the scalable env (ragged
+    existing cars, `cars[i].exist` read by the rollout, :489-507), 4 slots, 2 pedestrians."""
+    (tmp_path / "load_model" / "parameters").mkdir(parents=True)
+    monkeypatch.chdir(tmp_path)
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden", "gen"))
+    import refharness as R
+    from mhppo import envs
+    nc, npd, nl = 3, 2, 2
+    random.seed(10)
+    ref_env = R.make("scalable", nc, npd, nl)
+    with contextlib.redirect_stdout(io.StringIO()):
+        b_ref, w_ref = _train(ref_env, nc, nl, npd, driver="scalable")
+    fac = envs.make("Crosswalk_hybrid_multi_coop_scalable-v0", car_b=R.CAR_B, ped_b=R.PED_B, cross_b=R.CROSS_B,
+                    nb_car=nc, nb_ped=npd, nb_lines=nl, dt=0.3, max_episode=80, simulation="sin",
+                    backend=_HostBackend("scalable", nc, npd, nl, seed=10))
+    for k in ("car", "env", "ped"):
+        assert fac.observation_space[k].shape == ref_env.observation_space[k].shape
+    b_fac, w_fac = _train(fac, nc, nl, npd, driver="scalable")
     for x, y in zip(b_ref, b_fac):
         assert np.array_equal(x, y)
     for x, y in zip(w_ref, w_fac):

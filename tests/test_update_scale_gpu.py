@@ -1,0 +1,73 @@
+"""The fused training kernel at the bench's scale: one epoch of the critic and of the
+continuous actor (mhppo_mlp_train kinds 0 and 1) on the bench workload's real bucketed
+batch (4cars 4/1/2, 65 536 envs x 80 steps -> the cross head's ~10.5 M rows, 2 048
+per-wave partial gradients folded by k_grad_stage1/2) against a float64 torch autograd of
+the same losses (train_model_c, Coop-MH-PPO-scalable.py:778-815) on the same weights.
+Bar: max|dg| <= 1e-4 max|g| for every gradient; the loss sums within 1e-6 relative (the
+advantage sum, which cancels, within 1e-6 of sum|A|)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _f64(net):
+    from mhppo.models import Model_PPO
+    m = Model_PPO(net.n_in, net.n_out, net.model_type, mean=net.mean, std=net.std).double().cuda()
+    m.load_state_dict({k: v.double() for k, v in net.state_dict().items()})
+    return m
+
+
+def _flat_grad(net, loss):
+    gs = torch.autograd.grad(loss, [p for lay in (net.layer1, net.layer2, net.layer3, net.layer4)
+                                    for p in (lay.weight, lay.bias)])
+    return torch.cat([g.reshape(-1) for g in gs])
+
+
+def test_fused_epoch_at_bench_scale_vs_float64_autograd():
+    from mhppo import ppo
+    from mhppo.algo import Algo_PPO
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import bucket_segments
+    venv = VecCrosswalk("4cars", 65536, 4, 1, 2, seed_base=0)
+    torch.manual_seed(0)
+    algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
+    with torch.no_grad():
+        batch = algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0)
+    c, _, _ = bucket_segments(batch)
+    obs, act, lp, ret = c["obs"], c["act"], c["logp"], c["ret"]
+    M = obs.shape[0]
+    assert M > 5_000_000
+    m = float(M)
+    # ---- critic pass (kind 0): MSE gradient, (sum (V-G)^2, sum A, sum A^2), V
+    critic, actor = algo.critic_net_cross, algo.actor_net_cross
+    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+    gc, sc = gc.clone(), sc.clone()
+    c64 = _f64(critic)
+    V64 = torch.squeeze(c64(obs.double()), -1)
+    G = ret.double()
+    mse = ((V64 - G) ** 2).sum()
+    g64 = _flat_grad(c64, mse / m)
+    assert float((gc.double() - g64).abs().max()) <= 1e-4 * float(g64.abs().max())
+    assert abs(float(sc[0]) - float(mse)) <= 1e-6 * float(mse)
+    A64 = G - V64
+    assert abs(float(sc[1]) - float(A64.sum())) <= 1e-6 * float(A64.abs().sum())
+    assert abs(float(sc[2]) - float((A64 * A64).sum())) <= 1e-6 * float((A64 * A64).sum())
+    # ---- actor pass (kind 1): clip surrogate against A normalised with the epoch's critic
+    stats = sc[1:3].clone()
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, V, act, lp, stats, m_global=m)
+    ga = ga.clone()
+    a64 = _f64(actor)
+    mean = float(stats[0]) / m
+    std = ((float(stats[1]) - float(stats[0]) * mean) / (m - 1)) ** 0.5
+    A = ((G - V.double()) - mean) / (std + 1e-10)
+    mu = torch.squeeze(a64(obs.double()), -1)
+    x = (act.double() - mu) / (0.5 ** 0.5)
+    logp = -0.5 * (x * x + torch.log(torch.tensor(2 * torch.pi, dtype=torch.float64))) - 0.5 * torch.log(
+        torch.tensor(0.5, dtype=torch.float64))
+    r = torch.exp(logp - lp.double())
+    surr = -torch.minimum(r * A, r.clamp(0.8, 1.2) * A)
+    g64 = _flat_grad(a64, surr.sum() / m)
+    assert float((ga.double() - g64).abs().max()) <= 1e-4 * float(g64.abs().max())
+    assert abs(float(sa[0]) - float(surr.sum())) <= 1e-6 * float(surr.abs().sum())
