@@ -11,16 +11,33 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+class _F64(torch.nn.Module):
+    """Model_PPO's forward (Coop-MH-PPO-scalable.py:70-93) in float64 on the same weights."""
+
+    def __init__(self, net):
+        super().__init__()
+        self.kind, self.mean, self.std = net.model_type, net.mean, net.std
+        self.layers = torch.nn.ModuleList()
+        for lay in (net.layer1, net.layer2, net.layer3, net.layer4):
+            m = torch.nn.Linear(lay.in_features, lay.out_features, dtype=torch.float64, device=lay.weight.device)
+            with torch.no_grad():
+                m.weight.copy_(lay.weight.double())
+                m.bias.copy_(lay.bias.double())
+            self.layers.append(m)
+
+    def forward(self, x):
+        for m in self.layers[:3]:
+            x = torch.relu(m(x))
+        y = self.layers[3](x)
+        return torch.tanh(y) * self.std + self.mean if self.kind == 1 else y
+
+
 def _f64(net):
-    from mhppo.models import Model_PPO
-    m = Model_PPO(net.n_in, net.n_out, net.model_type, mean=net.mean, std=net.std).double().cuda()
-    m.load_state_dict({k: v.double() for k, v in net.state_dict().items()})
-    return m
+    return _F64(net)
 
 
 def _flat_grad(net, loss):
-    gs = torch.autograd.grad(loss, [p for lay in (net.layer1, net.layer2, net.layer3, net.layer4)
-                                    for p in (lay.weight, lay.bias)])
+    gs = torch.autograd.grad(loss, [p for m in net.layers for p in (m.weight, m.bias)])
     return torch.cat([g.reshape(-1) for g in gs])
 
 
