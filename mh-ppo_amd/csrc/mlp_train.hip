@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "../../include/mhppo.h"
@@ -613,6 +615,534 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   }
 }
 
+// =====================================================================================
+// Split-precision path of the 13-input heads (critic / continuous actor, the big batches).
+// Every GEMM of the pass runs on bf16 MFMA (v_mfma_f32_32x32x16_bf16: 16x the f32-MFMA
+// rate) with each f32 operand split EXACTLY into three bf16 parts, x = hi + mid + lo
+// (round-to-nearest at each level: |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|), and the six
+// products of combined order <= 2 accumulated in f32: the dropped terms are <= 2^-24
+// relative, i.e. the accuracy of an f32 product (the f32-MFMA kernel above stays the exact
+// k-ordered-fmaf reference, MHPPO_TRAIN_EXACT_F32).
+// Orientation as above (activations transposed, C registers of one layer = B operand of
+// the next with the permuted k order feature(16s + 8(j>>2) + 4h + (j&3)) of register
+// 8s + j).  Weights: row-major bf16 images [out][in] per part in LDS with padded rows (odd
+// multiples of 8 bytes: conflict-free row reads, linear addresses): the forward A fragments
+// are two 8-byte row reads, the backward (W^T) ones two ds_read_b64_tr_b16 transposed reads
+// of the same image.  Weight gradients sum over the tile's 32 rows: both operands go
+// through one per-wave bf16 image [row][feature] of the split parts, read back transposed.
+// Bias gradients and dW4 are f32 row sums through the same LDS slot.
+namespace x3 {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+struct F3 {  // one MFMA operand fragment (8 elements) as its three bf16 parts
+  u32x4 p[3];
+};
+
+constexpr int NIN = NIN_CONT;
+// row strides (bytes) of the bf16 images: odd multiples of 8 B over the data width
+constexpr int W1_ROWB = 40, W2_ROWB = 72, W3_ROWB = 136, IM_ROWB = 72;
+constexpr int W1_PART = 32 * W1_ROWB, W2_PART = 64 * W2_ROWB, W3_PART = 32 * W3_ROWB, IM_PART = 32 * IM_ROWB;
+constexpr int IMG = 3 * IM_PART;    // one tile image (three parts) = the per-wave LDS slot
+constexpr int TS = 36;              // f32 transpose image row stride (floats; 16-B aligned rows)
+static_assert(32 * TS * 4 <= IMG, "the f32 image shares the slot");
+constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_F = O_W3 + 3 * W3_PART;
+constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
+constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
+using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_DACC + 96 * 8;
+template <int WAVES>
+constexpr int lds_bytes() { return O_WAVE + WAVES * WAVE_B; }
+static_assert(lds_bytes<8>() <= 160 * 1024, "LDS budget");
+static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
+
+#ifdef MHPPO_X3_PHASE
+__device__ __forceinline__ void x3_phase() { __builtin_amdgcn_sched_barrier(0); }
+#else
+__device__ __forceinline__ void x3_phase() {}
+#endif
+// LDS image round trips within one wave: a wave's LDS instructions execute in issue order,
+// so only the compiler must keep the write -> read order (no lgkmcnt drain)
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
+  bf16x2 v = {(__bf16)x, (__bf16)y};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// (x, y) -> three packed bf16 pairs, x = hi + mid + lo exactly (element 0 in the low half)
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t &h, uint32_t &m, uint32_t &lo) {
+  h = pk_bf16(x, y);
+  const float x1 = x - __uint_as_float(h << 16), y1 = y - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(x1, y1);
+  const float x2 = x1 - __uint_as_float(m << 16), y2 = y1 - __uint_as_float(m & 0xffff0000u);
+  lo = pk_bf16(x2, y2);
+}
+// fragment element j = v[j]
+__device__ __forceinline__ F3 split8(const float *v) {
+  F3 f;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t a, b, c;
+    split_pair(v[2 * q], v[2 * q + 1], a, b, c);
+    f.p[0][q] = a;
+    f.p[1][q] = b;
+    f.p[2][q] = c;
+  }
+  return f;
+}
+// K-step s of a C tile (registers 8s .. 8s+7) as a B (or A) fragment
+__device__ __forceinline__ F3 split_step(const f32x16 &c, int s) {
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) v[q] = c[8 * s + q];
+  return split8(v);
+}
+
+__device__ __forceinline__ f32x16 mfma_b(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                  0, 0);
+}
+// C += A B on split operands: the six products of combined order <= 2, smallest first
+__device__ __forceinline__ f32x16 mfma6(const F3 &a, const F3 &b, f32x16 c) {
+  c = mfma_b(a.p[2], b.p[0], c);
+  c = mfma_b(a.p[0], b.p[2], c);
+  c = mfma_b(a.p[1], b.p[1], c);
+  c = mfma_b(a.p[1], b.p[0], c);
+  c = mfma_b(a.p[0], b.p[1], c);
+  return mfma_b(a.p[0], b.p[0], c);
+}
+
+__device__ __forceinline__ f32x4 mfma_b16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                  0, 0);
+}
+__device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
+  c = mfma_b16(a.p[2], b.p[0], c);
+  c = mfma_b16(a.p[0], b.p[2], c);
+  c = mfma_b16(a.p[1], b.p[1], c);
+  c = mfma_b16(a.p[1], b.p[0], c);
+  c = mfma_b16(a.p[0], b.p[1], c);
+  return mfma_b16(a.p[0], b.p[0], c);
+}
+__device__ __forceinline__ uint2 lds_u2(const char *p) { return *reinterpret_cast<const uint2 *>(p); }
+__device__ __forceinline__ uint2 tr16(const char *p) {
+  v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16 *)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+// two 8-byte reads (at p and p + du) of each part -> fragment elements 0-3 / 4-7
+template <int PART>
+__device__ __forceinline__ F3 rd_pair(const char *p, int du) {
+  F3 f;
+#pragma unroll
+  for (int pt = 0; pt < 3; pt++) {
+    const uint2 a = lds_u2(p + pt * PART), b = lds_u2(p + pt * PART + du);
+    f.p[pt] = u32x4{a.x, a.y, b.x, b.y};
+  }
+  return f;
+}
+template <int PART>
+__device__ __forceinline__ F3 tr_pair(const char *p, int du) {
+  F3 f;
+#pragma unroll
+  for (int pt = 0; pt < 3; pt++) {
+    const uint2 a = tr16(p + pt * PART), b = tr16(p + pt * PART + du);
+    f.p[pt] = u32x4{a.x, a.y, b.x, b.y};
+  }
+  return f;
+}
+// Lane address bases (loop invariants; every fragment is base + a compile-time offset):
+//  row read   (forward A of W, lane row r, half h): r * ROWB + 8 h; K-step s, u -> + 8 (4s + 2u)
+//  transposed (W^T A / image B, lane 16G + 4q + p): (4 (G>>1) + q) * ROWB... see below
+// Forward A fragment of W (rows `out` = base row + 32 t), K-step s, permuted k order:
+// element j <- in feature 16s + 8(j>>2) + 4h + (j&3), i.e. 8-byte chunk 4s + 2u + h.
+template <int ROWB, int PART>
+__device__ __forceinline__ F3 w_fwd(const char *rowbase, int t, int s) {
+  return rd_pair<PART>(rowbase + t * 32 * ROWB + 32 * s, 16);
+}
+// Backward A fragment of W^T (lane: in feature 32t + (l & 31)), K-step s over the out
+// features in the permuted order: element j <- W[16s + 8(j>>2) + 4h + (j&3)][in]; lane
+// 4q + p of group G addresses row 16s + 8u + 4(G>>1) + q, chunk 8t + 4(G&1) + p
+// (trbase = W + (4 (G>>1) + q) * ROWB + 8 (4 (G&1) + p)).
+template <int ROWB, int PART>
+__device__ __forceinline__ F3 w_bwd(const char *trbase, int t, int s) {
+  return tr_pair<PART>(trbase + 16 * s * ROWB + 64 * t, 8 * ROWB);
+}
+// Tile image [32 rows][32 features] of a C tile given as its two split K-step fragments:
+// lane (row r, half h) writes register group g (features 8g + 4h .. +3) as chunk 2g + h
+// (wbase = img + r * IM_ROWB + 8 h).
+__device__ __forceinline__ void img_write(char *wbase, const F3 &f0, const F3 &f1) {
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const F3 &f = g < 2 ? f0 : f1;
+    const int q = 2 * (g & 1);
+#pragma unroll
+    for (int pt = 0; pt < 3; pt++)
+      *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
+  }
+}
+// K-step s (rows 16s .. 16s+15) of the image read transposed: lane (feature l & 31, half h)
+// gets rows 16s + 8h + j, j = 0..7; lane 4q + p of group G addresses row 16s + 8(G>>1) +
+// 4u + q, chunk 4(G&1) + p (rbase = img + (8 (G>>1) + q) * IM_ROWB + 8 (4 (G&1) + p)).
+__device__ __forceinline__ F3 img_read(const char *rbase, int s) {
+  return tr_pair<IM_PART>(rbase + 16 * s * IM_ROWB, 4 * IM_ROWB);
+}
+// f32 transpose image T[feature][row] (stride TS) of a C tile, and the half-row sum of
+// feature (l & 31) over rows 16h .. 16h+15 (the halves are combined once, at the end)
+__device__ __forceinline__ void put_t(float *T, const f32x16 &v, int l) {
+  float *b = T + 4 * (l >> 5) * TS + (l & 31);  // lane base; register r at a constant offset
+#pragma unroll
+  for (int r = 0; r < 16; r++) b[((r & 3) + 8 * (r >> 2)) * TS] = v[r];
+}
+__device__ __forceinline__ float half_row_sum(const float *T, int l) {
+  const float4 *p = reinterpret_cast<const float4 *>(T + (l & 31) * TS + 16 * (l >> 5));
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const float4 v = p[c];
+    s += v.x;
+    s += v.y;
+    s += v.z;
+    s += v.w;
+  }
+  return s;
+}
+// stage one f32 weight element (split) into a row-major bf16 image
+__device__ __forceinline__ void stage_w(char *Wimg, int part, int rowb, int row, int col, float w) {
+  const __bf16 hi = (__bf16)w;
+  const float r1 = w - (float)hi;
+  const __bf16 mid = (__bf16)r1;
+  const __bf16 lo = (__bf16)(r1 - (float)mid);
+  const int off = row * rowb + col * 2;
+  *reinterpret_cast<__bf16 *>(Wimg + off) = hi;
+  *reinterpret_cast<__bf16 *>(Wimg + part + off) = mid;
+  *reinterpret_cast<__bf16 *>(Wimg + 2 * part + off) = lo;
+}
+// Hide a tile's values from common-subexpression elimination: the compiler would otherwise
+// keep a forward-pass split (1.5x the registers of the f32 tile) alive until the identical
+// split for the backward image, instead of the f32 tile it needs anyway for the ReLU masks.
+__device__ __forceinline__ void opaque(f32x16 &v) {
+#pragma unroll
+  for (int r = 0; r < 16; r++) asm volatile("" : "+v"(v[r]));
+}
+// d = (h > 0) ? d : 0 (ReLU derivative)
+__device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
+#pragma unroll
+  for (int r = 0; r < 16; r++) d[r] = h[r] > 0.0f ? d[r] : 0.0f;
+}
+}  // namespace x3
+
+// WAVES = 8: two waves per SIMD (256 registers each); 4: one wave per SIMD (512 registers)
+template <int KIND, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES)
+    k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
+                   float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
+                   const double *__restrict__ stats, double m_global, float out_mean, float out_std,
+                   float *__restrict__ gpart, double *__restrict__ dpart) {
+  using namespace x3;
+  extern __shared__ float lds[];
+  char *L8 = reinterpret_cast<char *>(lds);
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int nin = NIN;
+  constexpr int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
+                G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
+  // ---- stage the weights: bf16 images (three parts), b1 as input column 13 of W1
+  for (int i = tid; i < 32 * 16; i += 64 * WAVES) {
+    const int r = i >> 4, c = i & 15;
+    const float v = c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f);
+    stage_w(L8 + O_W1, W1_PART, W1_ROWB, r, c, v);
+  }
+  for (int i = tid; i < 64 * 32; i += 64 * WAVES) stage_w(L8 + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, W[G_W2 + i]);
+  for (int i = tid; i < 32 * 64; i += 64 * WAVES) stage_w(L8 + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, W[G_W3 + i]);
+  float *F = reinterpret_cast<float *>(L8 + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
+  for (int i = tid; i < NF; i += 64 * WAVES)
+    F[i] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
+  __syncthreads();
+  char *wb = L8 + O_WAVE + w * WAVE_B;
+  float *T = reinterpret_cast<float *>(wb);
+  float *inb = reinterpret_cast<float *>(wb + O_IN);
+  const int j = l & 31, kh = l >> 5;
+  const int G = l >> 4, q4 = (l >> 2) & 3, p4 = l & 3;
+  // lane address bases (every fragment access below is base + a constant)
+  const char *w1row = L8 + O_W1 + j * W1_ROWB + 16 * kh;
+  const char *w2row = L8 + O_W2 + j * W2_ROWB + 8 * kh;
+  const char *w3row = L8 + O_W3 + j * W3_ROWB + 8 * kh;
+  const char *w2tr = L8 + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
+  const char *w3tr = L8 + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
+  char *imw = wb + j * IM_ROWB + 8 * kh;
+  const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
+  const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
+  const float b40 = F[128];
+  f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
+  f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float gB2a = 0.f, gB2b = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
+  double *dacc = reinterpret_cast<double *>(wb + O_DACC) + j;
+  if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
+  float meanf = 0.f, stdf = 1.f;
+  if (KIND != K_CRITIC) {
+    double mean = stats[0] / m_global;
+    double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
+    meanf = (float)mean;
+    stdf = (float)sqrt(var > 0 ? var : 0.0);
+  }
+  const double inv_m = 1.0 / m_global;
+  const int64_t ntiles = (M + 31) / 32, nfull = M / 32;
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+
+  int cb = 0;
+  if (gw < nfull) prefetch_tile<KIND, LY>(inb, X, ret, V, act, lp_old, gw * 32, l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
+    const int64_t row0 = tile * 32;
+    const int nrows = (int)min((int64_t)32, M - row0);
+    float *slot = inb + cb * LY::IN_SZ;
+    const int64_t nxt = tile + nw;
+    if (nxt < nfull) {
+      prefetch_tile<KIND, LY>(inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
+      wait_vmcnt<prefetch_ops<KIND>()>();
+    } else if (tile < nfull) {
+      wait_vmcnt<0>();
+    } else {
+      load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
+    }
+    wave_sync();  // the tile's inputs have landed
+    const float *Xs = slot + LY::IN_X;
+    // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
+    auto layer1 = [&]() {
+      float v8[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        // row j, input column k = 8h + q (h = 1: columns 8..15; 13 is the bias input).  Columns
+        // 13-15 read the next row's first inputs (the slot's last row reads into its s0 block).
+        const int k = 8 * kh + q;
+        const float v = Xs[j * nin + 8 * kh + q];
+        v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
+      }
+      f32x16 h = mfma6(rd_pair<W1_PART>(w1row, 8), split8(v8), zero16());
+#pragma unroll
+      for (int r = 0; r < 16; r++) h[r] = relu0(h[r]);
+      return h;
+    };
+    f32x16 h1 = layer1();
+    x3_phase();
+    // ---- layer 2
+    f32x16 h2a = zero16(), h2b = zero16();
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const F3 b = split_step(h1, s);
+      h2a = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 0, s), b, h2a);
+      h2b = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 1, s), b, h2b);
+    }
+    bias_relu(h2a, F, kh);
+    bias_relu(h2b, F + 32, kh);
+    x3_phase();
+    // ---- layer 3
+    f32x16 h3 = zero16();
+#pragma unroll
+    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, s), split_step(h2a, s), h3);
+#pragma unroll
+    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, 2 + s), split_step(h2b, s), h3);
+    bias_relu(h3, F + 64, kh);
+    const float part0 = dot16(F + 96, h3, kh);
+    const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
+    x3_phase();
+    // ---- loss gradient dL/dy for this lane's row (as the f32 path)
+    const bool valid = j < nrows;
+    float dy0 = 0.0f;
+    if (valid) {
+      const float rt = slot[LY::IN_S0 + j];
+      if constexpr (KIND == K_CRITIC) {
+        const float v = y0;
+        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
+        const float a = rt - v;
+        const float d = v - rt;
+        if (kh == 0) {
+          dacc[0] += (double)d * (double)d;
+          dacc[32] += (double)a;
+          dacc[64] += (double)a * (double)a;
+        }
+        dy0 = (float)(2.0 * inv_m * (double)d);
+      } else {
+        const float t = tanhf(y0);
+        const float mu = t * out_std + out_mean;
+        const float a = rt - slot[LY::IN_S0 + 32 + j];
+        const float A = (a - meanf) / (stdf + 1e-10f);
+        const float diff = (float)((double)slot[LY::IN_S1 + j] - (double)mu);
+        const float x = diff * MVN_INV_L;
+        const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
+        const double r = exp((double)lp - (double)slot[LY::IN_S1 + 32 + j]);
+        double dfdr;
+        const double f = surr_and_grad(r, (double)A, dfdr);
+        if (kh == 0) dacc[0] += f;
+        const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+        dy0 = (dmu * out_std) * (1.0f - t * t);
+      }
+    }
+    gB4 += (kh == 0) ? dy0 : 0.0f;
+    // ---- layer 4 backward: dW4 = row sums of dy h3; d3 = dH3^T masked; dB3 = row sums of d3
+    f32x16 g, d3;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const float4 c = reinterpret_cast<const float4 *>(F + 96)[2 * q + kh];
+      const float cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = 4 * q + i;
+        g[r] = dy0 * h3[r];
+        d3[r] = (h3[r] > 0.0f) ? cw[i] * dy0 : 0.0f;
+      }
+    }
+    put_t(T, g, l);
+    lds_order();
+    gW4 += half_row_sum(T, l);
+    lds_order();
+    put_t(T, d3, l);
+    lds_order();
+    gB3 += half_row_sum(T, l);
+    lds_order();
+    x3_phase();
+    // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
+    const F3 d3f0 = split_step(d3, 0), d3f1 = split_step(d3, 1);
+    if constexpr (WAVES == 8) {
+      opaque(h2a);
+      opaque(h2b);
+    }
+    img_write(imw, d3f0, d3f1);
+    lds_order();
+    const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
+    lds_order();
+    img_write(imw, split_step(h2a, 0), split_step(h2a, 1));
+    lds_order();
+    gW3a = mfma6(ad0, img_read(imr, 0), gW3a);
+    gW3a = mfma6(ad1, img_read(imr, 1), gW3a);
+    lds_order();
+    img_write(imw, split_step(h2b, 0), split_step(h2b, 1));
+    lds_order();
+    gW3b = mfma6(ad0, img_read(imr, 0), gW3b);
+    gW3b = mfma6(ad1, img_read(imr, 1), gW3b);
+    lds_order();
+    x3_phase();
+    // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
+    f32x16 d2a = zero16(), d2b = zero16();
+    d2a = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 0, 0), d3f0, d2a);
+    d2a = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 0, 1), d3f1, d2a);
+    d2b = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 1, 0), d3f0, d2b);
+    d2b = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 1, 1), d3f1, d2b);
+    relu_mask(d2a, h2a);
+    relu_mask(d2b, h2b);
+    put_t(T, d2a, l);
+    lds_order();
+    gB2a += half_row_sum(T, l);
+    lds_order();
+    put_t(T, d2b, l);
+    lds_order();
+    gB2b += half_row_sum(T, l);
+    lds_order();
+    x3_phase();
+    // two waves per SIMD: h1 is recomputed here rather than held through layers 2-3 (registers)
+    if constexpr (WAVES == 8) {
+      lds_order();
+      h1 = layer1();
+    }
+    // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0
+    f32x16 d1 = zero16();
+    {
+      const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
+      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 0), f0, d1);
+      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 1), f1, d1);
+      // ---- dW2 (first half): sum over rows of d2a (x) h1: B = h1 image, A = d2a image
+      img_write(imw, split_step(h1, 0), split_step(h1, 1));
+      lds_order();
+      const F3 bh0 = img_read(imr, 0), bh1 = img_read(imr, 1);
+      lds_order();
+      img_write(imw, f0, f1);
+      lds_order();
+      gW2a = mfma6(img_read(imr, 0), bh0, gW2a);
+      gW2a = mfma6(img_read(imr, 1), bh1, gW2a);
+      lds_order();
+      const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
+      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 2), f2, d1);
+      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 3), f3, d1);
+      img_write(imw, f2, f3);
+      lds_order();
+      gW2b = mfma6(img_read(imr, 0), bh0, gW2b);
+      gW2b = mfma6(img_read(imr, 1), bh1, gW2b);
+      lds_order();
+    }
+    relu_mask(d1, h1);
+    x3_phase();
+    // ---- dW1 = sum over rows of d1 (x) [X | 1]: A = d1 image, B = the input rows (column 13:
+    // the constant 1, i.e. dB1)
+    // 16x16x32 tiles (out features 16t..16t+15 x input columns 0..15, all 32 rows in one
+    // K-step): lane l of group G = l >> 4 holds rows 8G..8G+7 of column l & 15 / feature l & 15
+    img_write(imw, split_step(d1, 0), split_step(d1, 1));
+    lds_order();
+    {
+      float xv[8];
+      const int n = l & 15;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const float v = Xs[(8 * G + q) * nin + (n < nin ? n : 0)];
+        xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
+      }
+      const F3 b = split8(xv);
+      gW1t[0] = mfma6_16(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
+      gW1t[1] = mfma6_16(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
+    }
+    lds_order();
+    x3_phase();
+  }
+  // ---- write this wave's partial gradient (packed torch layout)
+  float *gp = gpart + (size_t)gw * NWP;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int f = feat(r, l);
+    gp[G_W2 + f * 32 + j] = gW2a[r];
+    gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
+    gp[G_W3 + f * 64 + j] = gW3a[r];
+    gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
+  }
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int f = 16 * t + 4 * G + r, n = l & 15;
+      if (n < nin) gp[G_W1 + f * nin + n] = gW1t[t][r];
+      if (n == nin) gp[G_B1 + f] = gW1t[t][r];
+    }
+  }
+  // halves of the row sums: lanes j and j + 32 hold rows 0-15 / 16-31 of feature j
+  gB2a += __shfl_xor(gB2a, 32);
+  gB2b += __shfl_xor(gB2b, 32);
+  gB3 += __shfl_xor(gB3, 32);
+  gW4 += __shfl_xor(gW4, 32);
+  if (kh == 0) {
+    gp[G_B2 + j] = gB2a;
+    gp[G_B2 + 32 + j] = gB2b;
+    gp[G_B3 + j] = gB3;
+    gp[G_W4 + j] = gW4;
+  }
+  float b4s0 = gB4;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  if (kh == 0) s0 = dacc[0], s1 = dacc[32], s2 = dacc[64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o);
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (l == 0) {
+    gp[G_B4] = b4s0;
+    dpart[gw * 3 + 0] = s0;
+    dpart[gw * 3 + 1] = s1;
+    dpart[gw * 3 + 2] = s2;
+  }
+}
+
 // Deterministic two-stage gradient reduction over the per-wave partials (fixed order,
 // float64): stage 1 sums contiguous groups of waves, stage 2 sums the RG group totals.
 // Slot k < np is gradient k, slots np..np+2 the float64 sums.
@@ -665,6 +1195,17 @@ void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int n
 }
 }  // namespace
 
+// waves per block of the split-precision kernel: 8 (two per SIMD) or 4 (one per SIMD, 512
+// registers); MHPPO_X3_WAVES overrides for A/B runs
+int x3_waves() {
+  static int w = 0;
+  if (!w) {
+    const char *e = getenv("MHPPO_X3_WAVES");
+    w = (e && atoi(e) == 8) ? 8 : 4;  // 8 (two waves per SIMD) once its loop fits 256 registers
+  }
+  return w;
+}
+
 #ifdef MHPPO_TIMING
 // A/B timing builds only (not in include/mhppo.h): copy out and clear this TU's g_timing
 extern "C" int mhppo_debug_timing_train(unsigned long long *out16) {
@@ -680,8 +1221,10 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
                                float *value, const float *act, const float *logp_old, const double *stats,
                                const double *counts, double m_global, float out_mean, float out_std, float *grad,
                                double *sums, void *stream) {
+  const bool exact = (kind & MHPPO_TRAIN_EXACT_F32) != 0;
+  kind &= ~MHPPO_TRAIN_EXACT_F32;
   if (!grad || M < 0 || kind < K_CRITIC || kind > K_CHOICE || n_in < 1 || n_in > NIN_MAX)
-    return set_error(MHPPO_EINVAL, "bad argument (kind 0..2, 1 <= n_in <= %d)", NIN_MAX);
+    return set_error(MHPPO_EINVAL, "bad argument (kind 0..2 [| MHPPO_TRAIN_EXACT_F32], 1 <= n_in <= %d)", NIN_MAX);
   hipStream_t s = (hipStream_t)stream;
   if (M == 0) {  // an empty shard (data parallel): zero gradient, sums unchanged; X/ret/value may be NULL
     CHECK_HIP(hipMemsetAsync(grad, 0, sizeof(float) * n_params(n_in, kind == K_CHOICE ? 2 : 1), s));
@@ -704,7 +1247,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     wk.cus = cus;
   }
-  const int waves = pf ? 8 : 4;
+  const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
+  const int waves = split ? x3_waves() : (pf ? 8 : 4);
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
   const int64_t tiles = (M + 31) / 32;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
@@ -723,7 +1267,19 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   }
   const dim3 grid((unsigned)blocks);
 #define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
-  if (pf) {
+  if (split) {
+#define X3_LAUNCH(KIND_, W_)                                                                                  \
+  hipLaunchKernelGGL((k_mlp_train_x3<KIND_, W_>), grid, dim3(64 * W_), x3::lds_bytes<W_>(), s, packed, X, M, ret, \
+                     value, act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
+    if (x3_waves() == 4) {
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 4);
+      else X3_LAUNCH(K_CONT, 4);
+    } else {
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 8);
+      else X3_LAUNCH(K_CONT, 8);
+    }
+#undef X3_LAUNCH
+  } else if (pf) {
     if (kind == K_CRITIC)
       launch<K_CRITIC, 7, true>(MLP_ARGS);
     else

@@ -161,13 +161,18 @@ FLOPS_PER_ROW_CONT = flops_per_row(13, 1)
 N_IN_MAX = 64  # the fused kernel's widest input (scalable 8-slot choice head: dc = 54)
 
 KIND_CRITIC, KIND_CONT, KIND_CHOICE = 0, 1, 2
+TRAIN_EXACT_F32 = 0x100  # MHPPO_TRAIN_EXACT_F32: the f32-MFMA kernel (k-ordered fmaf sums) for the 13-input heads
+# When True, every fused pass uses the exact f32-MFMA kernel instead of the split-precision
+# bf16 one (include/mhppo.h mhppo_mlp_train); Algo_PPO(exact_f32=True) sets it.
+EXACT_F32 = False
 
 
 def n_params(n_in, n_out):
     return 32 * n_in + 32 + 64 * 32 + 64 + 32 * 64 + 32 + 32 * n_out + n_out
 
 
-def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=None, counts=None, m_global=1.0):
+def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=None, counts=None, m_global=1.0,
+                exact=None):
     """Fused forward/loss/backward of one head (mhppo_mlp_train).
     kind 0 (critic): returns (grad, sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
     kind 1 (continuous actor) / 2 (choice actor): returns (grad, sums[3] = (sum surrogate, 0, 0), None).
@@ -197,9 +202,10 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     if TRAIN_EVENTS is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
+    flags = TRAIN_EXACT_F32 if (EXACT_F32 if exact is None else exact) else 0
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().mhppo_mlp_train(
-            kind, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts),
+            kind | flags, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts),
             float(m_global), float(net.mean), float(net.std), p(grad), p(sums), _lib.stream_ptr()))
     if ev is not None:
         ev[1].record()

@@ -14,7 +14,9 @@ from mhppo.models import Model_PPO  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10485760)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--exact", action="store_true", help="the exact f32-MFMA kernel (MHPPO_TRAIN_EXACT_F32)")
 a = ap.parse_args()
+ppo.EXACT_F32 = a.exact
 M = a.rows
 torch.manual_seed(0)
 actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
