@@ -22,7 +22,11 @@ Extra JSON fields:
   roofline     — the dominant kernel, the fused continuous-head train kernel (k_mlp_train,
                  ~85 % of GPU time): algorithmic FLOPs per row x rows /
                  launch duration, from HIP events on its stream inside the timed region,
-                 summed over all launches; f32 MFMA peak 157.3 TFLOP/s.
+                 summed over all launches.  The kernel runs the bf16x3 split path
+                 (six bf16 MFMAs per f32 product, f32-level accuracy), so its
+                 ceiling is the bf16 dense MFMA peak / 6 = 419.4 TFLOP/s of f32-equivalent
+                 work; the fraction of the f32-MFMA peak (157.3) is reported beside it.
+                 With MHPPO_TRAIN_EXACT_F32 (ppo.EXACT_F32) the peak is the f32 one.
   roofline_env — the fused sample+env-step kernel: SURVEY §8(d)'s algorithmic bytes per
                  env-step (cfg3 1515 B, cfg4 1615 B) x N / its mean duration; 8 TB/s.
   cpu_baseline — the C oracle (same env + rollout, glibc, OpenMP over envs on the box's
@@ -45,7 +49,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec at 65536 envs × 4 agents, 1/2/4/8 MI355X + %HBM roofline"
 HBM_PEAK_GBS = 8000.0
-F32_MFMA_PEAK_TFLOPS = 157.3
+F32_MFMA_PEAK_TFLOPS = 157.3   # 256 CU x 4 SIMD x 64 FLOP/clk (32x32x2 f32) x 2.4 GHz
+X3_MFMA_PEAK_TFLOPS = 2516.6 / 6  # bf16 32x32x16: 1024 FLOP/clk/SIMD; six per split product
 CONFIGS = {3: ("4cars", 4, 1, 2), 4: ("scalable", 8, 1, 4), 2: ("coop", 2, 1, 2)}
 
 
@@ -204,7 +209,10 @@ def main():
     tr_rows = sum(m for _, _, m, _, _ in tr)
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
-    traffic = pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>")
+    split = not ppo.EXACT_F32
+    peak = X3_MFMA_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
+    traffic = (pmc_traffic("k_mlp_train_x3<0", "k_mlp_train_x3<1") if split else
+               pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>"))
     traffic_env = pmc_traffic("k_sample_env")
     agents = "ragged 1-8 existing of 8 slots" if variant == "scalable" else S
     line = {
@@ -217,9 +225,13 @@ def main():
                    "envs_per_gpu": N, "agents": agents, "T": T, "parallelism": f"dp{world}"},
         "dist": {"world_size": world, "backend": (a.dist_backend if world > 1 else None),
                  "env_ranges": [[r * N, (r + 1) * N] for r in range(world)]},
-        "roofline": {"bound": "mfma", "kernel": "k_mlp_train (fused continuous-head fwd/loss/bwd/wgrad, f32 MFMA)",
-                     "achieved": tr_tflops, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": tr_tflops / F32_MFMA_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "B/launch",
+        "roofline": {"bound": "mfma",
+                     "kernel": ("k_mlp_train_x3 (fused continuous-head fwd/loss/bwd/wgrad, bf16x3-split MFMA, "
+                                "f32-equivalent FLOPs)" if split else
+                                "k_mlp_train (fused continuous-head fwd/loss/bwd/wgrad, f32 MFMA)"),
+                     "achieved": tr_tflops, "peak": peak, "unit": "TFLOP/s",
+                     "frac": tr_tflops / peak, "frac_of_f32_mfma_peak": tr_tflops / F32_MFMA_PEAK_TFLOPS,
+                     "traffic": traffic, "traffic_unit": "B/launch",
                      "flops_per_row": ppo.FLOPS_PER_ROW_CONT, "rows_per_launch": tr_rows / max(len(tr), 1),
                      "launches": len(tr), "launch_ms": tr_ms / max(len(tr), 1)},
         "roofline_env": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,

@@ -100,6 +100,18 @@ __device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
 #else
 __device__ __forceinline__ void phase() {}
 #endif
+// wave-uniform values pinned to SGPRs (the compiler otherwise holds some in VGPRs)
+__device__ __forceinline__ float uniform_f(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
+  const uint64_t u = (uint64_t)x;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double uniform_d(double x) {
+  return __longlong_as_double(uniform_i64(__double_as_longlong(x)));
+}
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -653,7 +665,9 @@ constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_
 constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
 constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
-constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_DACC + 96 * 8;
+constexpr int H_PART = 16 * IM_ROWB;  // half image (16 rows) of dW3's A operand, two-wave kernel
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, O_H = O_DACC + 96 * 8,
+              WAVE_B = O_H + 3 * H_PART;
 template <int WAVES>
 constexpr int lds_bytes() { return O_WAVE + WAVES * WAVE_B; }
 static_assert(lds_bytes<8>() <= 160 * 1024, "LDS budget");
@@ -727,6 +741,29 @@ __device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
   c = mfma_b16(a.p[0], b.p[1], c);
   return mfma_b16(a.p[0], b.p[0], c);
 }
+// Weight-gradient accumulation C += A B (six products, as mfma6) with the accumulator pinned
+// to AGPRs: it is touched by nothing but these MFMAs inside the loop, so it never moves
+// between the register files and the arch VGPRs stay free for the tile's values.  Written as
+// one asm block: "s_nop 1" covers the VALU-write -> MFMA-read hazard on A / B (the compiler
+// cannot see the MFMAs inside), and back-to-back accumulation into the same AGPRs needs none.
+#ifndef MHPPO_X3_NO_AACC
+#define X3_MACC6(OP)                                                                                 \
+  asm("s_nop 1\n\t" OP " %0, %3, %4, %0\n\t" OP " %0, %1, %6, %0\n\t" OP " %0, %2, %5, %0\n\t" OP  \
+      " %0, %2, %4, %0\n\t" OP " %0, %1, %5, %0\n\t" OP " %0, %1, %4, %0"                              \
+      : "+a"(c)                                                                                      \
+      : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2]))
+__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6("v_mfma_f32_32x32x16_bf16"); }
+__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6("v_mfma_f32_16x16x32_bf16"); }
+#undef X3_MACC6
+// before the accumulators are read: the last MFMA's result latency (>= 18 passes)
+__device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
+}
+#else
+__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { c = mfma6(a, b, c); }
+__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { c = mfma6_16(a, b, c); }
+__device__ __forceinline__ void macc_drain(f32x16 &, f32x16 &, f32x16 &, f32x16 &, f32x4 &, f32x4 &) {}
+#endif
 __device__ __forceinline__ uint2 lds_u2(const char *p) { return *reinterpret_cast<const uint2 *>(p); }
 __device__ __forceinline__ uint2 tr16(const char *p) {
   v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16 *)(p));
@@ -773,6 +810,7 @@ __device__ __forceinline__ F3 w_bwd(const char *trbase, int t, int s) {
 // Tile image [32 rows][32 features] of a C tile given as its two split K-step fragments:
 // lane (row r, half h) writes register group g (features 8g + 4h .. +3) as chunk 2g + h
 // (wbase = img + r * IM_ROWB + 8 h).
+template <int PART = IM_PART>
 __device__ __forceinline__ void img_write(char *wbase, const F3 &f0, const F3 &f1) {
 #pragma unroll
   for (int g = 0; g < 4; g++) {
@@ -780,7 +818,7 @@ __device__ __forceinline__ void img_write(char *wbase, const F3 &f0, const F3 &f
     const int q = 2 * (g & 1);
 #pragma unroll
     for (int pt = 0; pt < 3; pt++)
-      *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
+      *reinterpret_cast<uint2 *>(wbase + pt * PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
   }
 }
 // K-step s (rows 16s .. 16s+15) of the image read transposed: lane (feature l & 31, half h)
@@ -866,16 +904,68 @@ __global__ void __launch_bounds__(64 * WAVES)
   float *inb = reinterpret_cast<float *>(wb + O_IN);
   const int j = l & 31, kh = l >> 5;
   const int G = l >> 4, q4 = (l >> 2) & 3, p4 = l & 3;
-  // lane address bases (every fragment access below is base + a constant)
-  const char *w1row = L8 + O_W1 + j * W1_ROWB + 16 * kh;
-  const char *w2row = L8 + O_W2 + j * W2_ROWB + 8 * kh;
-  const char *w3row = L8 + O_W3 + j * W3_ROWB + 8 * kh;
-  const char *w2tr = L8 + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *w3tr = L8 + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
-  char *imw = wb + j * IM_ROWB + 8 * kh;
-  const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
-  const float b40 = F[128];
+  // Lane address bases: every fragment access is base + a constant.  With two waves per SIMD
+  // (256 registers) the bases are not held through the loop but rebuilt where used from a lane
+  // id the compiler cannot hoist (LN): a few VALU per use instead of ~20 loop-long registers.
+  auto LN = [&]() {
+    int v = l;
+    if constexpr (WAVES == 8) asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto tr_off = [](int li, int rowb) {  // ds_read_b64_tr_b16 lane (4q + p of group G), 32x32x16 A/B
+    return (4 * ((li >> 5)) + ((li >> 2) & 3)) * rowb + 8 * (4 * ((li >> 4) & 1) + (li & 3));
+  };
+  auto w1row = [&]() { const int li = LN(); return (const char *)(L8 + O_W1 + (li & 31) * W1_ROWB + 16 * (li >> 5)); };
+  auto w2row = [&]() { const int li = LN(); return (const char *)(L8 + O_W2 + (li & 31) * W2_ROWB + 8 * (li >> 5)); };
+  auto w3row = [&]() { const int li = LN(); return (const char *)(L8 + O_W3 + (li & 31) * W3_ROWB + 8 * (li >> 5)); };
+  auto w2tr = [&]() { return (const char *)(L8 + O_W2 + tr_off(LN(), W2_ROWB)); };
+  auto w3tr = [&]() { return (const char *)(L8 + O_W3 + tr_off(LN(), W3_ROWB)); };
+  auto imw = [&]() { const int li = LN(); return wb + (li & 31) * IM_ROWB + 8 * (li >> 5); };
+  // image reads: rows 8 (G >> 1) + 4u + q (tr_off with a doubled row step)
+  auto imr = [&]() {
+    const int li = LN();
+    return (const char *)(wb + (8 * (li >> 5) + ((li >> 2) & 3)) * IM_ROWB + 8 * (4 * ((li >> 4) & 1) + (li & 3)));
+  };
+  auto imr16 = [&]() {  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
+    const int li = LN();
+    return (const char *)(wb + (8 * (li >> 4) + ((li >> 2) & 3)) * IM_ROWB + 8 * (li & 3));
+  };
+  const float b40 = uniform_f(F[128]);
+  // One wave per SIMD (512 registers): the weight fragments are loop invariants, read from LDS
+  // once here instead of once per tile (LDS instruction issue is the CU-shared resource)
+#ifdef MHPPO_X3_HOIST_FWD
+  constexpr bool HF = WAVES == 4;
+#else
+  constexpr bool HF = false;
+#endif
+  constexpr bool HB = WAVES == 4;  // measured: -3 % (the forward ones as well spill kind 1)
+  F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
+  if constexpr (HF) {
+    for (int t = 0; t < 2; t++)
+      for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row(), t, s);
+    for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row(), 0, s);
+  }
+  if constexpr (HB) {
+    for (int t = 0; t < 2; t++)
+      for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr(), t, s);
+    for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr(), 0, s);
+  }
+  auto fw2 = [&](int t, int s) -> F3 {
+    if constexpr (HF) return wf2[t][s];
+    else return w_fwd<W2_ROWB, W2_PART>(w2row(), t, s);
+  };
+  auto fw3 = [&](int s) -> F3 {
+    if constexpr (HF) return wf3[s];
+    else return w_fwd<W3_ROWB, W3_PART>(w3row(), 0, s);
+  };
+  auto bw3 = [&](int t, int s) -> F3 {
+    if constexpr (HB) return wb3[t][s];
+    else return w_bwd<W3_ROWB, W3_PART>(w3tr(), t, s);
+  };
+  auto bw2 = [&](int s) -> F3 {
+    if constexpr (HB) return wb2[s];
+    else return w_bwd<W2_ROWB, W2_PART>(w2tr(), 0, s);
+  };
   f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
   f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float gB2a = 0.f, gB2b = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
@@ -885,11 +975,11 @@ __global__ void __launch_bounds__(64 * WAVES)
   if (KIND != K_CRITIC) {
     double mean = stats[0] / m_global;
     double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
-    meanf = (float)mean;
-    stdf = (float)sqrt(var > 0 ? var : 0.0);
+    meanf = uniform_f((float)mean);
+    stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
   }
-  const double inv_m = 1.0 / m_global;
-  const int64_t ntiles = (M + 31) / 32, nfull = M / 32;
+  const double inv_m = uniform_d(1.0 / m_global);
+  const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
 
   int cb = 0;
@@ -912,15 +1002,16 @@ __global__ void __launch_bounds__(64 * WAVES)
     // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
     auto layer1 = [&]() {
       float v8[8];
+      const int li = LN();
 #pragma unroll
       for (int q = 0; q < 8; q++) {
         // row j, input column k = 8h + q (h = 1: columns 8..15; 13 is the bias input).  Columns
         // 13-15 read the next row's first inputs (the slot's last row reads into its s0 block).
-        const int k = 8 * kh + q;
-        const float v = Xs[j * nin + 8 * kh + q];
+        const int k = 8 * (li >> 5) + q;
+        const float v = Xs[(li & 31) * nin + 8 * (li >> 5) + q];
         v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
       }
-      f32x16 h = mfma6(rd_pair<W1_PART>(w1row, 8), split8(v8), zero16());
+      f32x16 h = mfma6(rd_pair<W1_PART>(w1row(), 8), split8(v8), zero16());
 #pragma unroll
       for (int r = 0; r < 16; r++) h[r] = relu0(h[r]);
       return h;
@@ -932,20 +1023,20 @@ __global__ void __launch_bounds__(64 * WAVES)
 #pragma unroll
     for (int s = 0; s < 2; s++) {
       const F3 b = split_step(h1, s);
-      h2a = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 0, s), b, h2a);
-      h2b = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 1, s), b, h2b);
+      h2a = mfma6(fw2(0, s), b, h2a);
+      h2b = mfma6(fw2(1, s), b, h2b);
     }
-    bias_relu(h2a, F, kh);
-    bias_relu(h2b, F + 32, kh);
+    bias_relu(h2a, F, LN() >> 5);
+    bias_relu(h2b, F + 32, LN() >> 5);
     x3_phase();
     // ---- layer 3
     f32x16 h3 = zero16();
 #pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, s), split_step(h2a, s), h3);
+    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(s), split_step(h2a, s), h3);
 #pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, 2 + s), split_step(h2b, s), h3);
-    bias_relu(h3, F + 64, kh);
-    const float part0 = dot16(F + 96, h3, kh);
+    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(2 + s), split_step(h2b, s), h3);
+    bias_relu(h3, F + 64, LN() >> 5);
+    const float part0 = dot16(F + 96, h3, LN() >> 5);
     const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
     x3_phase();
     // ---- loss gradient dL/dy for this lane's row (as the f32 path)
@@ -985,7 +1076,7 @@ __global__ void __launch_bounds__(64 * WAVES)
     f32x16 g, d3;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const float4 c = reinterpret_cast<const float4 *>(F + 96)[2 * q + kh];
+      const float4 c = reinterpret_cast<const float4 *>(F + 96)[2 * q + (LN() >> 5)];
       const float cw[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -994,13 +1085,13 @@ __global__ void __launch_bounds__(64 * WAVES)
         d3[r] = (h3[r] > 0.0f) ? cw[i] * dy0 : 0.0f;
       }
     }
-    put_t(T, g, l);
+    put_t(T, g, LN());
     lds_order();
-    gW4 += half_row_sum(T, l);
+    gW4 += half_row_sum(T, LN());
     lds_order();
-    put_t(T, d3, l);
+    put_t(T, d3, LN());
     lds_order();
-    gB3 += half_row_sum(T, l);
+    gB3 += half_row_sum(T, LN());
     lds_order();
     x3_phase();
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
@@ -1009,36 +1100,62 @@ __global__ void __launch_bounds__(64 * WAVES)
       opaque(h2a);
       opaque(h2b);
     }
-    img_write(imw, d3f0, d3f1);
-    lds_order();
-    const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
-    lds_order();
-    img_write(imw, split_step(h2a, 0), split_step(h2a, 1));
-    lds_order();
-    gW3a = mfma6(ad0, img_read(imr, 0), gW3a);
-    gW3a = mfma6(ad1, img_read(imr, 1), gW3a);
-    lds_order();
-    img_write(imw, split_step(h2b, 0), split_step(h2b, 1));
-    lds_order();
-    gW3b = mfma6(ad0, img_read(imr, 0), gW3b);
-    gW3b = mfma6(ad1, img_read(imr, 1), gW3b);
-    lds_order();
+    if constexpr (WAVES == 8) {
+      // registers: one K-step of the A operand at a time, staged through the half image H
+      // (rows 16s..16s+15 of d3, written by the lanes holding those rows) while the slot holds
+      // the B image: h2a (s = 0, 1), then h2b (s = 1 with the A fragment kept, then s = 0)
+      auto d3_half = [&](int s) {
+        if ((j >> 4) == s) img_write<H_PART>(imw() + O_H - 16 * IM_ROWB * s, d3f0, d3f1);
+        lds_order();
+        const F3 a = tr_pair<H_PART>(imr() + O_H, 4 * IM_ROWB);
+        lds_order();
+        return a;
+      };
+      img_write(imw(), split_step(h2a, 0), split_step(h2a, 1));
+      lds_order();
+      F3 ad = d3_half(0);
+      macc6(ad, img_read(imr(), 0), gW3a);
+      ad = d3_half(1);
+      macc6(ad, img_read(imr(), 1), gW3a);
+      lds_order();
+      img_write(imw(), split_step(h2b, 0), split_step(h2b, 1));
+      lds_order();
+      macc6(ad, img_read(imr(), 1), gW3b);
+      ad = d3_half(0);
+      macc6(ad, img_read(imr(), 0), gW3b);
+      lds_order();
+    } else {
+      img_write(imw(), d3f0, d3f1);
+      lds_order();
+      const F3 ad0 = img_read(imr(), 0), ad1 = img_read(imr(), 1);
+      lds_order();
+      img_write(imw(), split_step(h2a, 0), split_step(h2a, 1));
+      lds_order();
+      macc6(ad0, img_read(imr(), 0), gW3a);
+      macc6(ad1, img_read(imr(), 1), gW3a);
+      lds_order();
+      img_write(imw(), split_step(h2b, 0), split_step(h2b, 1));
+      lds_order();
+      macc6(ad0, img_read(imr(), 0), gW3b);
+      macc6(ad1, img_read(imr(), 1), gW3b);
+      lds_order();
+    }
     x3_phase();
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
     f32x16 d2a = zero16(), d2b = zero16();
-    d2a = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 0, 0), d3f0, d2a);
-    d2a = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 0, 1), d3f1, d2a);
-    d2b = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 1, 0), d3f0, d2b);
-    d2b = mfma6(w_bwd<W3_ROWB, W3_PART>(w3tr, 1, 1), d3f1, d2b);
+    d2a = mfma6(bw3(0, 0), d3f0, d2a);
+    d2a = mfma6(bw3(0, 1), d3f1, d2a);
+    d2b = mfma6(bw3(1, 0), d3f0, d2b);
+    d2b = mfma6(bw3(1, 1), d3f1, d2b);
     relu_mask(d2a, h2a);
     relu_mask(d2b, h2b);
-    put_t(T, d2a, l);
+    put_t(T, d2a, LN());
     lds_order();
-    gB2a += half_row_sum(T, l);
+    gB2a += half_row_sum(T, LN());
     lds_order();
-    put_t(T, d2b, l);
+    put_t(T, d2b, LN());
     lds_order();
-    gB2b += half_row_sum(T, l);
+    gB2b += half_row_sum(T, LN());
     lds_order();
     x3_phase();
     // two waves per SIMD: h1 is recomputed here rather than held through layers 2-3 (registers)
@@ -1050,25 +1167,25 @@ __global__ void __launch_bounds__(64 * WAVES)
     f32x16 d1 = zero16();
     {
       const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
-      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 0), f0, d1);
-      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 1), f1, d1);
+      d1 = mfma6(bw2(0), f0, d1);
+      d1 = mfma6(bw2(1), f1, d1);
       // ---- dW2 (first half): sum over rows of d2a (x) h1: B = h1 image, A = d2a image
-      img_write(imw, split_step(h1, 0), split_step(h1, 1));
+      img_write(imw(), split_step(h1, 0), split_step(h1, 1));
       lds_order();
-      const F3 bh0 = img_read(imr, 0), bh1 = img_read(imr, 1);
+      const F3 bh0 = img_read(imr(), 0), bh1 = img_read(imr(), 1);
       lds_order();
-      img_write(imw, f0, f1);
+      img_write(imw(), f0, f1);
       lds_order();
-      gW2a = mfma6(img_read(imr, 0), bh0, gW2a);
-      gW2a = mfma6(img_read(imr, 1), bh1, gW2a);
+      macc6(img_read(imr(), 0), bh0, gW2a);
+      macc6(img_read(imr(), 1), bh1, gW2a);
       lds_order();
       const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
-      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 2), f2, d1);
-      d1 = mfma6(w_bwd<W2_ROWB, W2_PART>(w2tr, 0, 3), f3, d1);
-      img_write(imw, f2, f3);
+      d1 = mfma6(bw2(2), f2, d1);
+      d1 = mfma6(bw2(3), f3, d1);
+      img_write(imw(), f2, f3);
       lds_order();
-      gW2b = mfma6(img_read(imr, 0), bh0, gW2b);
-      gW2b = mfma6(img_read(imr, 1), bh1, gW2b);
+      macc6(img_read(imr(), 0), bh0, gW2b);
+      macc6(img_read(imr(), 1), bh1, gW2b);
       lds_order();
     }
     relu_mask(d1, h1);
@@ -1077,24 +1194,25 @@ __global__ void __launch_bounds__(64 * WAVES)
     // the constant 1, i.e. dB1)
     // 16x16x32 tiles (out features 16t..16t+15 x input columns 0..15, all 32 rows in one
     // K-step): lane l of group G = l >> 4 holds rows 8G..8G+7 of column l & 15 / feature l & 15
-    img_write(imw, split_step(d1, 0), split_step(d1, 1));
+    img_write(imw(), split_step(d1, 0), split_step(d1, 1));
     lds_order();
     {
       float xv[8];
-      const int n = l & 15;
+      const int li = LN(), n = li & 15;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
-        const float v = Xs[(8 * G + q) * nin + (n < nin ? n : 0)];
+        const float v = Xs[(8 * (li >> 4) + q) * nin + (n < nin ? n : 0)];
         xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
       }
       const F3 b = split8(xv);
-      gW1t[0] = mfma6_16(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
-      gW1t[1] = mfma6_16(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
+      macc6_16(tr_pair<IM_PART>(imr16(), 4 * IM_ROWB), b, gW1t[0]);
+      macc6_16(tr_pair<IM_PART>(imr16() + 32, 4 * IM_ROWB), b, gW1t[1]);
     }
     lds_order();
     x3_phase();
   }
   // ---- write this wave's partial gradient (packed torch layout)
+  macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
   float *gp = gpart + (size_t)gw * NWP;
 #pragma unroll
   for (int r = 0; r < 16; r++) {

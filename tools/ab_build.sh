@@ -1,8 +1,6 @@
 #!/bin/bash
-# Build an alternative libmhppo.so for A/B kernel experiments:
-#   tools/ab_build.sh <name> "<extra hipcc flags>"  ->  build_ab/<name>/libmhppo.so
-# then run with MHPPO_LIB=build_ab/<name>/libmhppo.so (mhppo/_lib.py).
+# Build an A/B variant of libmhppo.so into build_ab/<name>/ with extra compiler flags.
+# usage: bash tools/ab_build.sh <name> "<flags>"
 set -e
-ROOT=$(cd "$(dirname "$0")/.." && pwd)
-NAME=$1; shift
-make -s -C "$ROOT/mh-ppo_amd/csrc" OUT="$ROOT/build_ab/$NAME/libmhppo.so" BUILD="$ROOT/build_ab/$NAME/obj" EXTRA="$*"
+make -s -C "$(dirname "$0")/../mh-ppo_amd/csrc" -j8 BUILD="$PWD/build_ab/$1/obj" OUT="$PWD/build_ab/$1/libmhppo.so" EXTRA="$2" 2>&1 | grep -E "error" || true
+ls -la build_ab/$1/libmhppo.so

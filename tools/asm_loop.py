@@ -22,7 +22,8 @@ def main(path, sub, top=30):
             t = mm.group(1) or mm.group(2)
             if t in labels and labels[t] < n:
                 loops.append((labels[t], n))
-    a, b = max(loops, key=lambda x: x[1] - x[0])
+    outer = [lp for lp in loops if "Loop Header: Depth=1" in body[lp[0]]]  # the tile loop, not
+    a, b = max(outer or loops, key=lambda x: x[1] - x[0])                 # structurizer back-jumps
     c = collections.Counter()
     for ln in body[a:b]:
         t = ln.strip().split(" ")[0]

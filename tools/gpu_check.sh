@@ -18,6 +18,6 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
   cat $OUT/bench_cfg4.json
 fi
 if [ "$WHAT" = prof ] || [ "$WHAT" = all ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || { echo PROF FAILED; tail -30 $OUT/prof.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || { echo PROF FAILED; tail -30 $OUT/prof.err; exit 1; }
   find $OUT/prof -name '*kernel_stats.csv' | head -3
 fi
