@@ -63,12 +63,16 @@ def env_step_bytes(S, P, A_ctl, obs_dim):
     return 2 * (S * 56 + P * 88 + 12) + (S * 2 + P * 78 + 12) + 4 * 2 * A_ctl + 4 * obs_dim + 8 * A_ctl + 1 + 8
 
 
+CONFIG = 3  # the workload of this run (set in main): PMC summaries are per config
+
+
 def pmc_traffic(*patterns):
     """Mean HBM bytes per launch over the kernels matching `patterns`, from the committed
-    rocprofv3 PMC summary (profiles/pmc_traffic.json, made by tools/pmc_summary.py from
+    rocprofv3 PMC summary of this config (profiles/pmc_traffic_cfg<N>.json, made by
+    tools/gpu_pmc.sh <tag> <config> -> tools/pmc_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes of this bench; reads = 2 x FETCH_SIZE on
     gfx950).  None when absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_cfg{CONFIG}.json")
     try:
         ks = json.load(open(path))["kernels"]
     except (OSError, ValueError, KeyError):
@@ -157,6 +161,8 @@ def main():
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
 
+    global CONFIG
+    CONFIG = a.config
     variant, nc, npd, nl = CONFIGS[a.config]
     N, T = a.envs, 80
     venv = VecCrosswalk(variant, N, nc, npd, nl, seed_base=0, env_id_offset=rank * N, device=f"cuda:{local}")

@@ -215,6 +215,19 @@ int mhppo_returns_scan(const double *rew, float *ret, int64_t B, int32_t T, doub
  * is column b; the rollout's rew buffer is [T, N*S]). */
 int mhppo_returns_scan_tm(const double *rew, float *ret, int64_t B, int32_t T, double gamma, void *stream);
 
+/* Segment-major buckets (bucket_segments; replaces the per-episode concatenation of
+ * Coop-MH-PPO-scalable.py:489-507).  Segment s < NS (= N*S records per step) with pos[s] >= 0
+ * belongs to bucket bucket[s] (0 or 1) at position pos[s]: its time-major records t < T
+ * (obs [.., 13] float32, act / logp / ret float32, rew float64; record t*NS + s) go to rows
+ * pos[s]*T + t of dst[bucket[s]] (caller-sized: count of segments x T rows). */
+typedef struct {
+  float *obs, *act, *logp, *ret;
+  double *rew;
+} mhppo_bucket_dst;
+int mhppo_bucket_scatter(const int64_t *pos, const int8_t *bucket, int64_t NS, int32_t T, const float *obs_tm,
+                         const float *act_tm, const float *logp_tm, const float *ret_tm, const double *rew_tm,
+                         const mhppo_bucket_dst *dst, void *stream);
+
 /* Advantage statistics of A = G - V over M rows: stats float64 [2] += (sum A, sum A^2)
  * (caller zeroes it; partial sums all-reduce across ranks).  Normalisation
  * A' = (A - mean) / (std_unbiased + 1e-10) with mean/std from (stats, M_global). */

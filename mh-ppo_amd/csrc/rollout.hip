@@ -630,6 +630,68 @@ __global__ void __launch_bounds__(TPB) k_returns(const double *rew, float *ret, 
 }
 
 // time-major records [T][B]: lane b scans column b (coalesced across the wave)
+// Segment-major buckets (bucket_segments; the reference's per-episode concatenation,
+// Coop-MH-PPO-scalable.py:489-507), both buckets in one pass over the time-major records:
+// record (t, s) of a segment s in bucket b = bucket[s] (pos[s] >= 0) goes to row pos[s]*T + t
+// of bucket b.  A block owns 64 segments x 16 steps: coalesced loads of the records (64
+// consecutive segments per step) into LDS, then each segment's 16 rows leave as contiguous
+// runs — every record read once and every bucket row written once, in full lines.
+namespace bk {
+constexpr int SEGS = 64, STEPS = 16;
+}
+__global__ void __launch_bounds__(TPB)
+    k_bucket_scatter(const int64_t *__restrict__ pos, const int8_t *__restrict__ bucket, int64_t NS, int T,
+                     const float *__restrict__ obs, const float *__restrict__ act, const float *__restrict__ logp,
+                     const float *__restrict__ ret, const double *__restrict__ rew, mhppo_bucket_dst d0,
+                     mhppo_bucket_dst d1) {
+  using namespace bk;
+  __shared__ float s_obs[SEGS * STEPS * NF_C];
+  __shared__ float s_v[3][SEGS * STEPS];
+  __shared__ double s_rew[SEGS * STEPS];
+  __shared__ int64_t s_pos[SEGS];
+  __shared__ int8_t s_b[SEGS];
+  const int64_t s0 = (int64_t)blockIdx.x * SEGS;
+  const int t0 = blockIdx.y * STEPS;
+  const int nseg = (int)min((int64_t)SEGS, NS - s0), nt = min(STEPS, T - t0);
+  const int tid = threadIdx.x;
+  if (tid < SEGS) {
+    s_pos[tid] = tid < nseg ? pos[s0 + tid] : -1;
+    s_b[tid] = tid < nseg ? bucket[s0 + tid] : 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < SEGS * STEPS; i += TPB) {  // i = step * SEGS + seg: lanes on consecutive segments
+    const int sg = i % SEGS, tl = i / SEGS;
+    if (sg >= nseg || tl >= nt || s_pos[sg] < 0) continue;
+    const int64_t rec = (int64_t)(t0 + tl) * NS + s0 + sg;
+    const int o = sg * STEPS + tl;  // LDS: segment-major
+    const float *so = obs + rec * NF_C;
+#pragma unroll
+    for (int j = 0; j < NF_C; j++) s_obs[o * NF_C + j] = so[j];
+    s_v[0][o] = act[rec];
+    s_v[1][o] = logp[rec];
+    s_v[2][o] = ret[rec];
+    s_rew[o] = rew[rec];
+  }
+  __syncthreads();
+  // each wave writes the runs of 16 segments: segment sg's rows pos*T + t0 .. + nt
+  const int w = tid >> 6, l = tid & 63;
+  for (int sg = w; sg < nseg; sg += TPB / 64) {
+    const int64_t p = s_pos[sg];
+    if (p < 0) continue;
+    const mhppo_bucket_dst &D = s_b[sg] ? d1 : d0;
+    const int64_t r0 = p * T + t0;
+    float *oo = D.obs + r0 * NF_C;
+    for (int j = l; j < nt * NF_C; j += 64) oo[j] = s_obs[sg * STEPS * NF_C + j];
+    if (l < nt) {
+      const int o = sg * STEPS + l;
+      D.act[r0 + l] = s_v[0][o];
+      D.logp[r0 + l] = s_v[1][o];
+      D.ret[r0 + l] = s_v[2][o];
+      D.rew[r0 + l] = s_rew[o];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(TPB) k_returns_tm(const double *rew, float *ret, int64_t B, int T, double gamma) {
   int64_t b = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (b >= B) return;
@@ -1003,6 +1065,22 @@ int mhppo_returns_scan_tm(const double *rew, float *ret, int64_t B, int32_t T, d
   if (!rew || !ret || B < 0 || T <= 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (B == 0) return MHPPO_OK;
   hipLaunchKernelGGL(k_returns_tm, grid_for(B), dim3(TPB), 0, (hipStream_t)stream, rew, ret, B, T, gamma);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_bucket_scatter(const int64_t *pos, const int8_t *bucket, int64_t NS, int32_t T, const float *obs_tm,
+                         const float *act_tm, const float *logp_tm, const float *ret_tm, const double *rew_tm,
+                         const mhppo_bucket_dst *dst, void *stream) {
+  if (NS < 0 || T <= 0 || !dst) return set_error(MHPPO_EINVAL, "bad argument");
+  if (NS == 0) return MHPPO_OK;
+  if (!pos || !bucket || !obs_tm || !act_tm || !logp_tm || !ret_tm || !rew_tm)
+    return set_error(MHPPO_EINVAL, "null pointer");
+  const int64_t nb = (NS + bk::SEGS - 1) / bk::SEGS;
+  if (nb > 0x7fffffff) return set_error(MHPPO_EINVAL, "too many segments");
+  dim3 g((unsigned)nb, (unsigned)((T + bk::STEPS - 1) / bk::STEPS));
+  hipLaunchKernelGGL(k_bucket_scatter, g, dim3(TPB), 0, (hipStream_t)stream, pos, bucket, NS, (int)T, obs_tm,
+                     act_tm, logp_tm, ret_tm, rew_tm, dst[0], dst[1]);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

@@ -32,6 +32,10 @@ class Mlp(ctypes.Structure):
                 ("mean", ctypes.c_float), ("std", ctypes.c_float)]
 
 
+class BucketDst(ctypes.Structure):  # mhppo_bucket_dst
+    _fields_ = [("obs", P), ("act", P), ("logp", P), ("ret", P), ("rew", P)]
+
+
 class RolloutBufs(ctypes.Structure):
     _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
                 ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
@@ -74,6 +78,7 @@ _SIGS = {
     "mhppo_philox_normal_2d": (I32, [U64, U64, U64, P, I64, I64, P]),
     "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_returns_scan_tm": (I32, [P, P, I64, I32, F64, P]),
+    "mhppo_bucket_scatter": (I32, [P, P, I64, I32] + [P] * 7),
     "mhppo_adv_stats": (I32, [P, P, I64, P, P]),
     "mhppo_adv_normalize": (I32, [P, P, I64, P, F64, P, P]),
     "mhppo_ppo_cont_fwd_bwd": (I32, [P, P, P, P, I64, F64, P, P, P]),

@@ -1,8 +1,10 @@
 """PPO update of the multi-head actor-critic (Algo_PPO.train_model_c / _d,
 Coop-MH-PPO-scalable.py:778-851), full batch, on the GPU.
 
-Every head's epoch runs on the fused f32-MFMA training kernel (mhppo_mlp_train,
-csrc/mlp_train.hip): a critic pass (forward, MSE gradient, advantage sums) and an
+Every head's epoch runs on the fused training kernel (mhppo_mlp_train, csrc/mlp_train.hip;
+the 13-input heads on its bf16x3 split-precision MFMA path — six bf16 products per f32
+product, f32-level accuracy — or, with EXACT_F32 / MHPPO_TRAIN_EXACT_F32, on f32 MFMA with
+k-ordered sums; the choice head on f32 MFMA): a critic pass (forward, MSE gradient, advantage sums) and an
 actor pass (forward, clip-surrogate gradient against the advantage normalised with
 the start-of-epoch critic, backward, weight gradients); Adam (fused) steps each net.
 Epoch semantics follow the reference: the advantage uses the critic of the start of

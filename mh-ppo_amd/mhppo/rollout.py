@@ -211,17 +211,9 @@ def bucket_segments(batch, fix_bucket=False):
     seg_wait = torch.nonzero(wait.reshape(-1)).squeeze(1)
     seg_all = torch.nonzero(exist.reshape(-1)).squeeze(1)
     ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
-    t_off = torch.arange(T, device=seg_all.device, dtype=torch.int64) * (N * S)
 
-    def rows(seg):
-        # row (segment k, step t) of the bucket = record t * N*S + seg[k]: segment-major order
-        idx = (seg.unsqueeze(1) + t_off.unsqueeze(0)).reshape(-1)
-        obs = batch.obs_c_tm.reshape(T * N * S, NF_C).index_select(0, idx)
-        act = batch.act_tm.reshape(-1).index_select(0, idx)
-        lp = batch.logp_tm.reshape(-1).index_select(0, idx)
-        rt = ret.reshape(-1).index_select(0, idx)
-        rw = batch.rew_tm.reshape(-1).index_select(0, idx)
-        return dict(obs=obs, act=act, logp=lp, ret=rt, rew=rw, n_seg=int(seg.numel()))
+    cross_r, wait_r = scatter_buckets(seg_cross, seg_wait, N * S, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm,
+                                      ret, batch.rew_tm)
 
     cl = batch.closest.reshape(N * S).long().index_select(0, seg_all)
     base = seg_all * P + cl
@@ -233,4 +225,28 @@ def bucket_segments(batch, fix_bucket=False):
         ret=batch.ep_min.reshape(-1).index_select(0, seg_all).float(),
         n_seg=int(seg_all.numel()),
     )
-    return rows(seg_cross), rows(seg_wait), choice
+    return cross_r, wait_r, choice
+
+
+def scatter_buckets(seg0, seg1, NS, T, obs_tm, act_tm, logp_tm, ret_tm, rew_tm):
+    """Two segment-major buckets of time-major records (mhppo_bucket_scatter): row
+    (k, t) = k*T + t of bucket b is record t*NS + seg_b[k] (segments disjoint)."""
+    dev = obs_tm.device
+    pos = torch.full((NS,), -1, dtype=torch.int64, device=dev)
+    bucket = torch.zeros(NS, dtype=torch.int8, device=dev)
+    outs, dst = [], (_lib.BucketDst * 2)()
+    for b, seg in enumerate((seg0, seg1)):
+        n = int(seg.numel())
+        pos[seg] = torch.arange(n, dtype=torch.int64, device=dev)
+        bucket[seg] = b
+        o = dict(obs=torch.empty(n * T, NF_C, dtype=torch.float32, device=dev),
+                 act=torch.empty(n * T, dtype=torch.float32, device=dev),
+                 logp=torch.empty(n * T, dtype=torch.float32, device=dev),
+                 ret=torch.empty(n * T, dtype=torch.float32, device=dev),
+                 rew=torch.empty(n * T, dtype=torch.float64, device=dev), n_seg=n)
+        dst[b] = _lib.BucketDst(*[o[k].data_ptr() for k in ("obs", "act", "logp", "ret", "rew")])
+        outs.append(o)
+    srcs = [x.contiguous() for x in (obs_tm, act_tm, logp_tm, ret_tm, rew_tm)]
+    _lib.check(_lib.lib().mhppo_bucket_scatter(_lib.ptr(pos), _lib.ptr(bucket), NS, T, *[_lib.ptr(x) for x in srcs],
+                                               dst, _lib.stream_ptr(device=dev)))
+    return outs
