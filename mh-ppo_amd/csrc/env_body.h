@@ -99,8 +99,8 @@ MHPPO_HD void car_init(EV &E, int s, double line, double offset, int exist) {
   E.car(C_PA, s) = 0.0;
   E.car(C_ES, s) = 0.0;
   E.car(C_TS, s) = (V == V_SCALABLE) ? 0. : -10.;
-  E.car(C_H0, s) = 0.;
-  E.car(C_H1, s) = 0.;
+  E.hist_nf(0) &= ~(int32_t)(1u << s);  // history = [0, 0]
+  E.hist_nf(1) &= ~(int32_t)(1u << s);
   E.car(C_LINE, s) = line;
   E.car(C_EXIST, s) = exist ? 1.0 : 0.0;
 }
@@ -160,6 +160,8 @@ template <int V>
 MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   // cross first: it sizes everything else (:844)
   Env<V> E(c, b, e);
+  E.hist_nf(0) = 0;  // every car's history = [0, 0] (car_init clears its own bits as well)
+  E.hist_nf(1) = 0;
   E.cross = E.rng.uniform(c.xb0, c.xb1);
   E.cl = (double)c.nb_lines * E.cross;
   b.envd[sidx(E_ND, E_CROSS, e)] = E.cross;

@@ -83,8 +83,11 @@ enum { V_COOP = 0, V_4CARS = 1, V_SCALABLE = 2, V_NAIF = 3, V_4CARS2 = 4, V_STOP
 // 4cars / 4cars2: nb_car AVs, each followed by an IDM car (4cars2: PPO-driven follower)
 constexpr bool has_followers(int v) { return v == V_4CARS || v == V_4CARS2; }
 
-// car fields (double) [C_NF][nC] per env (env-blocked, see sidx)
-enum { C_AC, C_VC, C_SC, C_LIGHT, C_PA, C_ES, C_TS, C_H0, C_H1, C_LINE, C_EXIST, C_NF };
+// car fields (double) [C_NF][nC] per env (env-blocked, see sidx).  The reference's two-step
+// acceleration history (car.step's discount_array = [1, 0, 0], :550, :643-645) enters the
+// acceleration only as 0 * h, i.e. only through whether h is finite: it is kept
+// as one non-finite bit per car and history step (envi EI_H0NF / EI_H1NF, bit s = car slot s).
+enum { C_AC, C_VC, C_SC, C_LIGHT, C_PA, C_ES, C_TS, C_LINE, C_EXIST, C_NF };
 // ped fields (double) [P_NF][P] per env
 enum { P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS, P_IVX, P_IVY, P_RATIO,
        P_CSTOP, P_A, P_B, P_W, P_NF };
@@ -99,7 +102,8 @@ enum : uint32_t {
 };
 // env scalars
 enum { E_CROSS, E_TIME, E_ND };
-enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_MTB, EI_NI };
+enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_MTB, EI_H0NF, EI_H1NF, EI_NI };
+constexpr int MAX_CAR_SLOTS = 32;  // the history bit words (AV slots + 4cars followers)
 
 struct Cfg {
   // nS: action slots (acc + light each); nAV: AV slots with rewards/detection (= nS except
@@ -324,6 +328,7 @@ struct Env {
   MHPPO_HD int nP() const { return c.P; }
   MHPPO_HD int ped_traffic() const { return b.envi[sidx(EI_NI, EI_PEDTRAF, e)]; }
   MHPPO_HD int car_traffic() const { return b.envi[sidx(EI_NI, EI_CARTRAF, e)]; }
+  MHPPO_HD int32_t &hist_nf(int k) const { return b.envi[sidx(EI_NI, EI_H0NF + k, e)]; }
 
   MHPPO_HD double &car(int f, int s) const { return b.car[sidx(C_NF * c.nC, f * c.nC + s, e)]; }
   MHPPO_HD double &pedf(int f, int p) const { return b.ped[sidx(P_NF * c.P, f * c.P + p, e)]; }
@@ -354,6 +359,7 @@ struct EnvR {
   mutable double car_[C_NF][NC];
   mutable double ped_[P_NF][NP];
   mutable uint32_t pfl_[NP];
+  mutable int32_t hnf_[2];
   int ptraf, ctraf;
 
   MHPPO_HD EnvR(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
@@ -363,6 +369,8 @@ struct EnvR {
     cl = (double)c.nb_lines * cross;
     ptraf = b.envi[sidx(EI_NI, EI_PEDTRAF, e)];
     ctraf = b.envi[sidx(EI_NI, EI_CARTRAF, e)];
+    hnf_[0] = b.envi[sidx(EI_NI, EI_H0NF, e)];
+    hnf_[1] = b.envi[sidx(EI_NI, EI_H1NF, e)];
 #pragma unroll
     for (int f = 0; f < C_NF; f++)
 #pragma unroll
@@ -379,13 +387,15 @@ struct EnvR {
   // dynamic fields only: line/exist and the pedestrian's static draws never change in a step
   MHPPO_HD void commit() {
     const size_t N = (size_t)c.N;
-    constexpr int dyn_car[6] = {C_AC, C_VC, C_SC, C_LIGHT, C_H0, C_H1};
+    constexpr int dyn_car[4] = {C_AC, C_VC, C_SC, C_LIGHT};
     constexpr int det_car[3] = {C_PA, C_ES, C_TS};
     constexpr int dyn_ped[10] = {P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS};
 #pragma unroll
-    for (int k = 0; k < 6; k++)
+    for (int k = 0; k < 4; k++)
 #pragma unroll
       for (int s = 0; s < NC; s++) b.car[sidx(C_NF * NC, dyn_car[k] * NC + s, e)] = car_[dyn_car[k]][s];
+    b.envi[sidx(EI_NI, EI_H0NF, e)] = hnf_[0];
+    b.envi[sidx(EI_NI, EI_H1NF, e)] = hnf_[1];
 #pragma unroll
     for (int k = 0; k < 3; k++)
 #pragma unroll
@@ -407,6 +417,7 @@ struct EnvR {
   MHPPO_HD int car_traffic() const { return ctraf; }
 
   MHPPO_HD double &car(int f, int s) const { return car_[f][s]; }
+  MHPPO_HD int32_t &hist_nf(int k) const { return hnf_[k]; }
   MHPPO_HD double &pedf(int f, int p) const { return ped_[f][p]; }
   MHPPO_HD uint32_t &pflag(int p) const { return pfl_[p]; }
 };
@@ -849,13 +860,15 @@ MHPPO_HD inline void car_step(const EV &E, int s, double action, double light) {
   else if (acc > 0) sg = 1;
   else sg = pymax(pymin(-Vc / (dt * acc), 1.), 0.);
   if (V == V_STOP && sg > 0.) acc = pymax(acc, -Vc / (dt * sg));  // stop :603-605
-  double h0 = E.car(C_H0, s), h1 = E.car(C_H1, s);
+  // fa = 0 + 1*acc + 0*h0 + 0*h1 (:643-645): 0.0 + acc is never -0, so a finite h adds an
+  // exact (signed) zero and changes nothing; a non-finite one makes fa NaN
+  const uint32_t bit = 1u << s;
+  const uint32_t h0nf = (uint32_t)E.hist_nf(0), h1nf = (uint32_t)E.hist_nf(1);
   double fa = 0.0;
   fa = fa + 1.0 * acc;
-  fa = fa + 0. * h0;
-  fa = fa + 0. * h1;
-  E.car(C_H1, s) = h0;
-  E.car(C_H0, s) = acc;
+  if ((h0nf | h1nf) & bit) fa = __builtin_nan("");
+  E.hist_nf(1) = (int32_t)((h1nf & ~bit) | (h0nf & bit));              // h1 <- h0
+  E.hist_nf(0) = (int32_t)((h0nf & ~bit) | (isfinite(acc) ? 0u : bit));  // h0 <- acc
   fa = fa * sg;
   double speed = Vc + dt * fa;
   double pos = (fa * E.c.dt2 / 2.0) + (Vc * dt) + (E.car(C_SC, s));

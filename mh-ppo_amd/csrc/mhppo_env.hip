@@ -116,6 +116,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
     return set_error(MHPPO_EINVAL, "bad nb_car/nb_ped/nb_lines");
   int nS = cfg->variant == V_SCALABLE ? 2 * cfg->nb_lines : (cfg->variant == V_4CARS2 ? 2 : 1) * cfg->nb_car;
   if (nS > MAXS) return set_error(MHPPO_EINVAL, "too many car slots (%d > %d)", nS, MAXS);
+  static_assert(2 * MAXS <= MAX_CAR_SLOTS, "history bit words");
   if (cfg->variant == V_SCALABLE && cfg->nb_car > nS)
     return set_error(MHPPO_EINVAL, "scalable: nb_car must be <= 2*nb_lines (random.sample)");
   if (cfg->variant == V_NAIF && nS > 16) return set_error(MHPPO_EINVAL, "naif: at most 16 cars");
