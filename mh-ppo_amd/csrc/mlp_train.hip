@@ -183,6 +183,29 @@ __device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
     v[4 * q + 3] = relu0(v[4 * q + 3] + c.w);
   }
 }
+// the C-layout broadcast of a per-feature vector b (register r of lane half kh = b[feature]):
+// a bias as an MFMA chain's initial accumulator, or w4 for the output layer
+__device__ __forceinline__ f32x16 feat_vec(const float *b, int kh) {
+  const float4 *b4 = reinterpret_cast<const float4 *>(b);
+  f32x16 v;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const float4 c = b4[2 * q + kh];
+    v[4 * q + 0] = c.x;
+    v[4 * q + 1] = c.y;
+    v[4 * q + 2] = c.z;
+    v[4 * q + 3] = c.w;
+  }
+  return v;
+}
+// ReLU of an MFMA result as one integer max on the bits (signed compare orders non-negative
+// floats like their values and sends every negative one, -0 included, to +0); fmaxf would
+// first canonicalize the register (a second VALU op per element)
+__device__ __forceinline__ float relu_bits(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+__device__ __forceinline__ void relu16(f32x16 &v) {
+#pragma unroll
+  for (int r = 0; r < 16; r++) v[r] = relu_bits(v[r]);
+}
 // sum_r w[feature(r, l)] * h[r] over this lane's 16 features
 __device__ __forceinline__ float dot16(const float *w, const f32x16 &h, int kh) {
   float part = 0.0f;
@@ -951,11 +974,8 @@ __global__ void __launch_bounds__(64 * WAVES)
   const float b40 = uniform_f(F[128]);
   // One wave per SIMD (512 registers): the weight fragments are loop invariants, read from LDS
   // once here instead of once per tile
-#ifdef MHPPO_X3_HOIST_FWD
-  constexpr bool HF = WAVES == 4 && NT == 1;
-#else
-  constexpr bool HF = false;
-#endif
+  // the forward ones too for the critic pass (the actor pass's loss needs those registers)
+  constexpr bool HF = WAVES == 4 && NT == 1 && KIND == K_CRITIC;
 #ifdef MHPPO_X3_NO_HOIST_BWD
   constexpr bool HB = false;
 #else
@@ -1050,8 +1070,7 @@ __global__ void __launch_bounds__(64 * WAVES)
         v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
       }
       f32x16 h = mfma6(rd_pair<W1_PART>(w1row(), 8), split8(v8), zero16());
-#pragma unroll
-      for (int r = 0; r < 16; r++) h[r] = relu0(h[r]);
+      relu16(h);
       return h;
     };
     f32x16 h1[NT], h2a[NT], h2b[NT], h3[NT], d3[NT], d2a[NT], d2b[NT], d1[NT];
@@ -1061,35 +1080,40 @@ __global__ void __launch_bounds__(64 * WAVES)
     for (int u = 0; u < NT; u++) h1[u] = layer1(u);
     x3_phase();
     // ---- layer 2
+    // the biases ride in as the chains' initial accumulators (no VALU adds, no LDS wait in the
+    // middle of the layer)
 #pragma unroll
     for (int u = 0; u < NT; u++) {
-      h2a[u] = zero16();
-      h2b[u] = zero16();
+      h2a[u] = feat_vec(F, LN() >> 5);
+      h2b[u] = feat_vec(F + 32, LN() >> 5);
 #pragma unroll
       for (int s = 0; s < 2; s++) {
         const F3 b = split_step(h1[u], s);
         h2a[u] = mfma6(fw2(0, s), b, h2a[u]);
         h2b[u] = mfma6(fw2(1, s), b, h2b[u]);
       }
-      bias_relu(h2a[u], F, LN() >> 5);
-      bias_relu(h2b[u], F + 32, LN() >> 5);
+      relu16(h2a[u]);
+      relu16(h2b[u]);
     }
     x3_phase();
     // ---- layer 3
 #pragma unroll
     for (int u = 0; u < NT; u++) {
-      h3[u] = zero16();
+      h3[u] = feat_vec(F + 64, LN() >> 5);
 #pragma unroll
       for (int s = 0; s < 2; s++) h3[u] = mfma6(fw3(s), split_step(h2a[u], s), h3[u]);
 #pragma unroll
       for (int s = 0; s < 2; s++) h3[u] = mfma6(fw3(2 + s), split_step(h2b[u], s), h3[u]);
-      bias_relu(h3[u], F + 64, LN() >> 5);
+      relu16(h3[u]);
     }
     x3_phase();
     // ---- loss gradient dL/dy for this lane's row (as the f32 path)
 #pragma unroll
     for (int u = 0; u < NT; u++) {
-      const float part0 = dot16(F + 96, h3[u], LN() >> 5);
+      const f32x16 w4v = feat_vec(F + 96, LN() >> 5);
+      float part0 = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) part0 = fmaf(w4v[r], h3[u][r], part0);
       const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
       const bool valid = j < nrows[u];
       const float *sl = slot[u];
@@ -1124,22 +1148,16 @@ __global__ void __launch_bounds__(64 * WAVES)
         }
       }
       gB4 += (kh == 0) ? dy0[u] : 0.0f;
+      // layer 4 backward: d3 = dH3^T masked (w4 as loaded for the output)
+#pragma unroll
+      for (int r = 0; r < 16; r++) d3[u][r] = (h3[u][r] > 0.0f) ? w4v[r] * dy0[u] : 0.0f;
     }
-    // ---- layer 4 backward: dW4 = row sums of dy h3; d3 = dH3^T masked; dB3 = row sums of d3
+    // ---- dW4 = row sums of dy h3; dB3 = row sums of d3
 #pragma unroll
     for (int u = 0; u < NT; u++) {
       f32x16 g;
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const float4 c = reinterpret_cast<const float4 *>(F + 96)[2 * q + (LN() >> 5)];
-        const float cw[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int r = 4 * q + i;
-          g[r] = dy0[u] * h3[u][r];
-          d3[u][r] = (h3[u][r] > 0.0f) ? cw[i] * dy0[u] : 0.0f;
-        }
-      }
+      for (int r = 0; r < 16; r++) g[r] = dy0[u] * h3[u][r];
       float *T = Tu(u);
       put_t(T, g, LN());
       lds_order();
