@@ -1349,346 +1349,6 @@ __global__ void __launch_bounds__(64 * WAVES)
   }
 }
 
-// Software-pipelined variant (one wave per SIMD): each loop iteration runs the BACKWARD of
-// tile i beside the FORWARD of tile i+1, phase by phase, so the wave's single in-order stream
-// always holds two independent dependency chains (the split arithmetic of one tile issues while
-// the other tile's MFMAs run) without doubling the live state the way two tiles in lock step
-// do.  Tile i's inputs stay in their slot until its backward (dW1 reads X): three input slots
-// rotate (backward, forward, DMA in flight).  The forward is branch-free (rows past M and the
-// dummy tile after a wave's last one contribute exact zeros), so an iteration is one block.
-namespace x3 {
-struct WS {  // per-wave LDS of the pipelined kernel
-  static constexpr int O_T = IMG_AL, O_IN = O_T + (32 * TS * 4 + 15) / 16 * 16, O_DACC = O_IN + 3 * LY::IN_SZ * 4,
-                       WAVE_B = O_DACC + 3 * 64 * 8;
-  static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
-};
-constexpr int lds_bytes_pipe() { return O_WAVE + 4 * WS::WAVE_B; }
-static_assert(lds_bytes_pipe() <= 160 * 1024, "LDS budget");
-}  // namespace x3
-
-template <int KIND>
-__global__ void __launch_bounds__(256)
-    k_mlp_train_x3s(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
-                    float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
-                    const double *__restrict__ stats, double m_global, float out_mean, float out_std,
-                    float *__restrict__ gpart, double *__restrict__ dpart) {
-  using namespace x3;
-  constexpr int WAVES = 4;
-  extern __shared__ float lds[];
-  char *L8 = reinterpret_cast<char *>(lds);
-  const int tid = threadIdx.x, l = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int nin = NIN;
-  constexpr int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
-                G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
-  for (int i = tid; i < 32 * 16; i += 64 * WAVES) {
-    const int r = i >> 4, c = i & 15;
-    const float v = c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f);
-    stage_w(L8 + O_W1, W1_PART, W1_ROWB, r, c, v);
-  }
-  for (int i = tid; i < 64 * 32; i += 64 * WAVES) stage_w(L8 + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, W[G_W2 + i]);
-  for (int i = tid; i < 32 * 64; i += 64 * WAVES) stage_w(L8 + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, W[G_W3 + i]);
-  float *F = reinterpret_cast<float *>(L8 + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
-  for (int i = tid; i < NF; i += 64 * WAVES)
-    F[i] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
-  __syncthreads();
-  char *wb = L8 + O_WAVE + w * WS::WAVE_B;
-  float *T = reinterpret_cast<float *>(wb + WS::O_T);
-  float *inb = reinterpret_cast<float *>(wb + WS::O_IN);
-  const int j = l & 31, kh = l >> 5;
-  const int G = l >> 4, q4 = (l >> 2) & 3, p4 = l & 3;
-  const char *w1row = L8 + O_W1 + j * W1_ROWB + 16 * kh;
-  const char *w2row = L8 + O_W2 + j * W2_ROWB + 8 * kh;
-  const char *w3row = L8 + O_W3 + j * W3_ROWB + 8 * kh;
-  const char *w2tr = L8 + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *w3tr = L8 + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
-  char *imw = wb + j * IM_ROWB + 8 * kh;
-  const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;
-  const float b40 = uniform_f(F[128]);
-  // the backward W^T fragments: loop invariants, read once
-  F3 wb3[2][2], wb2[4];
-  for (int t = 0; t < 2; t++)
-    for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
-  for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
-  f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
-  f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  float gB2a = 0.f, gB2b = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
-  double *dacc = reinterpret_cast<double *>(wb + WS::O_DACC) + l;  // [3][64]: lanes >= 32 add 0
-  dacc[0] = dacc[64] = dacc[128] = 0.0;
-  float meanf = 0.f, stdf = 1.f;
-  if (KIND != K_CRITIC) {
-    double mean = stats[0] / m_global;
-    double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
-    meanf = uniform_f((float)mean);
-    stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
-  }
-  const double inv_m = uniform_d(1.0 / m_global);
-  const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
-  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  auto slot_of = [&](int k) { return inb + k * LY::IN_SZ; };  // k = iteration index mod 3
-  auto nrows_of = [&](int64_t tile) { return (int)max((int64_t)0, min((int64_t)32, M - tile * 32)); };
-  // inputs of `tile` into slot k: DMA (full tiles, landed by a later wait) or plain loads
-  auto fetch = [&](int64_t tile, int k) {
-    if (tile < nfull) prefetch_tile<KIND, LY>(slot_of(k), X, ret, V, act, lp_old, tile * 32, l);
-    else load_tile_sync<KIND, LY>(slot_of(k), X, nin, ret, V, act, lp_old, tile * 32, nrows_of(tile), l);
-  };
-  // ---------------- forward of one tile: h1, h2a, h2b, the masked dH3 tile, loss bookkeeping
-  struct Fw {
-    f32x16 h1, h2a, h2b, d3;
-  };
-  auto fwd_l1 = [&](const float *sl, Fw &o) {
-    const float *Xs = sl + LY::IN_X;
-    float v8[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int k = 8 * kh + q;
-      const float v = Xs[j * nin + 8 * kh + q];
-      v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
-    }
-    o.h1 = mfma6(rd_pair<W1_PART>(w1row, 8), split8(v8), zero16());
-#pragma unroll
-    for (int r = 0; r < 16; r++) o.h1[r] = relu0(o.h1[r]);
-  };
-  auto fwd_l2 = [&](Fw &o) {
-    o.h2a = zero16();
-    o.h2b = zero16();
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const F3 b = split_step(o.h1, s);
-      o.h2a = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 0, s), b, o.h2a);
-      o.h2b = mfma6(w_fwd<W2_ROWB, W2_PART>(w2row, 1, s), b, o.h2b);
-    }
-    bias_relu(o.h2a, F, kh);
-    bias_relu(o.h2b, F + 32, kh);
-  };
-  auto fwd_l3 = [&](const Fw &o) {
-    f32x16 h3 = zero16();
-#pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, s), split_step(o.h2a, s), h3);
-#pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(w_fwd<W3_ROWB, W3_PART>(w3row, 0, 2 + s), split_step(o.h2b, s), h3);
-    bias_relu(h3, F + 64, kh);
-    return h3;
-  };
-  // loss gradient, branch-free; then dW4 / dB3 row sums and the masked d3 tile
-  auto fwd_loss = [&](const float *sl, int64_t row0, int nrows, const f32x16 &h3, Fw &o) {
-    const float part0 = dot16(F + 96, h3, kh);
-    const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
-    const bool valid = j < nrows;
-    const bool own = valid && kh == 0;  // one lane per row carries the row's loss sums
-    const float rt = sl[LY::IN_S0 + j];
-    float dy0;
-    if constexpr (KIND == K_CRITIC) {
-      const float v = y0;
-      // rows past M are outside the buffer range: the store is dropped (both lane halves write
-      // the same value to the same address)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 4 * nrows), 4 * j, 0, 0);
-      const float a = rt - v;
-      const float d = v - rt;
-      dacc[0] += own ? (double)d * (double)d : 0.0;
-      dacc[64] += own ? (double)a : 0.0;
-      dacc[128] += own ? (double)a * (double)a : 0.0;
-      dy0 = valid ? (float)(2.0 * inv_m * (double)d) : 0.0f;
-    } else {
-      const float t = tanhf(y0);
-      const float mu = t * out_std + out_mean;
-      const float a = rt - sl[LY::IN_S0 + 32 + j];
-      const float A = (a - meanf) / (stdf + 1e-10f);
-      const float diff = (float)((double)sl[LY::IN_S1 + j] - (double)mu);
-      const float x = diff * MVN_INV_L;
-      const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-      const double r = exp((double)lp - (double)sl[LY::IN_S1 + 32 + j]);
-      double dfdr;
-      const double f = surr_and_grad(r, (double)A, dfdr);
-      dacc[0] += own ? f : 0.0;
-      const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
-      dy0 = valid ? (dmu * out_std) * (1.0f - t * t) : 0.0f;
-    }
-    gB4 += (kh == 0) ? dy0 : 0.0f;
-    f32x16 g;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const float4 c = reinterpret_cast<const float4 *>(F + 96)[2 * q + kh];
-      const float cw[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int r = 4 * q + i;
-        g[r] = dy0 * h3[r];
-        o.d3[r] = (h3[r] > 0.0f) ? cw[i] * dy0 : 0.0f;
-      }
-    }
-    put_t(T, g, l);
-    lds_order();
-    gW4 += half_row_sum(T, l);
-    lds_order();
-    put_t(T, o.d3, l);
-    lds_order();
-    gB3 += half_row_sum(T, l);
-    lds_order();
-  };
-  // ---------------- backward of one tile (its forward state in b)
-  auto bwd_dw3 = [&](const Fw &b, F3 &d3f0, F3 &d3f1) {
-    d3f0 = split_step(b.d3, 0);
-    d3f1 = split_step(b.d3, 1);
-    img_write(imw, d3f0, d3f1);
-    lds_order();
-    const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
-    lds_order();
-    img_write(imw, split_step(b.h2a, 0), split_step(b.h2a, 1));
-    lds_order();
-    macc6<true>(ad0, img_read(imr, 0), gW3a);
-    macc6<true>(ad1, img_read(imr, 1), gW3a);
-    lds_order();
-    img_write(imw, split_step(b.h2b, 0), split_step(b.h2b, 1));
-    lds_order();
-    macc6<true>(ad0, img_read(imr, 0), gW3b);
-    macc6<true>(ad1, img_read(imr, 1), gW3b);
-    lds_order();
-  };
-  auto bwd_dh2 = [&](const Fw &b, const F3 &d3f0, const F3 &d3f1, f32x16 &d2a, f32x16 &d2b) {
-    d2a = zero16();
-    d2b = zero16();
-    d2a = mfma6(wb3[0][0], d3f0, d2a);
-    d2a = mfma6(wb3[0][1], d3f1, d2a);
-    d2b = mfma6(wb3[1][0], d3f0, d2b);
-    d2b = mfma6(wb3[1][1], d3f1, d2b);
-    relu_mask(d2a, b.h2a);
-    relu_mask(d2b, b.h2b);
-    put_t(T, d2a, l);
-    lds_order();
-    gB2a += half_row_sum(T, l);
-    lds_order();
-    put_t(T, d2b, l);
-    lds_order();
-    gB2b += half_row_sum(T, l);
-    lds_order();
-  };
-  auto bwd_dh1 = [&](const Fw &b, const f32x16 &d2a, const f32x16 &d2b) {
-    f32x16 d1 = zero16();
-    const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
-    d1 = mfma6(wb2[0], f0, d1);
-    d1 = mfma6(wb2[1], f1, d1);
-    img_write(imw, split_step(b.h1, 0), split_step(b.h1, 1));
-    lds_order();
-    const F3 bh0 = img_read(imr, 0), bh1 = img_read(imr, 1);
-    lds_order();
-    img_write(imw, f0, f1);
-    lds_order();
-    macc6<true>(img_read(imr, 0), bh0, gW2a);
-    macc6<true>(img_read(imr, 1), bh1, gW2a);
-    lds_order();
-    const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
-    d1 = mfma6(wb2[2], f2, d1);
-    d1 = mfma6(wb2[3], f3, d1);
-    img_write(imw, f2, f3);
-    lds_order();
-    macc6<true>(img_read(imr, 0), bh0, gW2b);
-    macc6<true>(img_read(imr, 1), bh1, gW2b);
-    lds_order();
-    relu_mask(d1, b.h1);
-    return d1;
-  };
-  auto bwd_dw1 = [&](const float *sl, const f32x16 &d1) {
-    img_write(imw, split_step(d1, 0), split_step(d1, 1));
-    lds_order();
-    const float *Xs = sl + LY::IN_X;
-    float xv[8];
-    const int n = l & 15;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const float v = Xs[(8 * G + q) * nin + (n < nin ? n : 0)];
-      xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
-    }
-    const F3 bx = split8(xv);
-    macc6_16<true>(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), bx, gW1t[0]);
-    macc6_16<true>(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), bx, gW1t[1]);
-    lds_order();
-  };
-
-  // ---------------- prologue: inputs of the wave's first two tiles, forward of the first
-  Fw cur;
-  if (gw < ntiles) {
-    fetch(gw, 0);
-    fetch(gw + nw, 1);
-    if (gw + nw < nfull) wait_vmcnt<prefetch_ops<KIND>()>();
-    else wait_vmcnt<0>();
-    wave_sync();
-    fwd_l1(slot_of(0), cur);
-    fwd_l2(cur);
-    const f32x16 h3 = fwd_l3(cur);
-    fwd_loss(slot_of(0), gw * 32, nrows_of(gw), h3, cur);
-  }
-  int k = 0;  // slot of the tile in backward; k+1, k+2 (mod 3): forward, in flight
-  for (int64_t tile = gw; tile < ntiles; tile += nw) {
-    const int kf = k == 2 ? 0 : k + 1, kp = kf == 2 ? 0 : kf + 1;
-    const int64_t nxt = tile + nw, nn = nxt + nw;  // nxt: forward here (a dummy past the end)
-    fetch(nn, kp);
-    if (nn < nfull) wait_vmcnt<prefetch_ops<KIND>()>();
-    else wait_vmcnt<0>();
-    wave_sync();  // tile nxt's inputs have landed
-    const float *sf = slot_of(kf), *sb = slot_of(k);
-    Fw nx;
-    F3 d3f0, d3f1;
-    f32x16 d2a, d2b;
-    fwd_l1(sf, nx);
-    bwd_dw3(cur, d3f0, d3f1);
-    fwd_l2(nx);
-    bwd_dh2(cur, d3f0, d3f1, d2a, d2b);
-    const f32x16 h3 = fwd_l3(nx);
-    const f32x16 d1 = bwd_dh1(cur, d2a, d2b);
-    fwd_loss(sf, nxt * 32, nrows_of(nxt), h3, nx);
-    bwd_dw1(sb, d1);
-    cur = nx;
-    k = kf;
-  }
-  // ---- write this wave's partial gradient (packed torch layout)
-  macc_drain<true>(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
-  float *gp = gpart + (size_t)gw * NWP;
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int f = feat(r, l);
-    gp[G_W2 + f * 32 + j] = gW2a[r];
-    gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
-    gp[G_W3 + f * 64 + j] = gW3a[r];
-    gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
-  }
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int f = 16 * t + 4 * G + r, n = l & 15;
-      if (n < nin) gp[G_W1 + f * nin + n] = gW1t[t][r];
-      if (n == nin) gp[G_B1 + f] = gW1t[t][r];
-    }
-  }
-  gB2a += __shfl_xor(gB2a, 32);
-  gB2b += __shfl_xor(gB2b, 32);
-  gB3 += __shfl_xor(gB3, 32);
-  gW4 += __shfl_xor(gW4, 32);
-  if (kh == 0) {
-    gp[G_B2 + j] = gB2a;
-    gp[G_B2 + 32 + j] = gB2b;
-    gp[G_B3 + j] = gB3;
-    gp[G_W4 + j] = gW4;
-  }
-  float b4s0 = gB4;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
-  double s0 = dacc[0], s1 = dacc[64], s2 = dacc[128];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s0 += __shfl_xor(s0, o);
-    s1 += __shfl_xor(s1, o);
-    s2 += __shfl_xor(s2, o);
-  }
-  if (l == 0) {
-    gp[G_B4] = b4s0;
-    dpart[gw * 3 + 0] = s0;
-    dpart[gw * 3 + 1] = s1;
-    dpart[gw * 3 + 2] = s2;
-  }
-}
 
 // Deterministic two-stage gradient reduction over the per-wave partials (fixed order,
 // float64): stage 1 sums contiguous groups of waves, stage 2 sums the RG group totals.
@@ -1761,16 +1421,6 @@ int x3_nt() {
   }
   return n;
 }
-// software-pipelined kernel (backward of tile i beside the forward of tile i+1; one wave per
-// SIMD): MHPPO_X3_PIPE=1 selects it (A/B runs)
-int x3_pipe() {
-  static int n = -1;
-  if (n < 0) {
-    const char *e = getenv("MHPPO_X3_PIPE");
-    n = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return n;
-}
 
 #ifdef MHPPO_TIMING
 // A/B timing builds only (not in include/mhppo.h): copy out and clear this TU's g_timing
@@ -1815,7 +1465,7 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   }
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
   const int waves = split ? x3_waves() : (pf ? 8 : 4);
-  const int nt = split && waves == 4 && !x3_pipe() ? x3_nt() : 1;  // tiles per wave and loop iteration
+  const int nt = split && waves == 4 ? x3_nt() : 1;  // tiles per wave and loop iteration
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over groups of nt 32-row tiles
   const int64_t groups = ((M + 31) / 32 + nt - 1) / nt;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (groups + waves - 1) / waves));
@@ -1838,14 +1488,7 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
 #define X3_LAUNCH(KIND_, W_, NT_)                                                                         \
   hipLaunchKernelGGL((k_mlp_train_x3<KIND_, W_, NT_>), grid, dim3(64 * W_), (x3::lds_bytes<W_, NT_>()), s, packed, \
                      X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
-    if (waves == 4 && x3_pipe()) {
-      if (kind == K_CRITIC)
-        hipLaunchKernelGGL((k_mlp_train_x3s<K_CRITIC>), grid, dim3(256), x3::lds_bytes_pipe(), s, packed, X, M, ret,
-                           value, act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d);
-      else
-        hipLaunchKernelGGL((k_mlp_train_x3s<K_CONT>), grid, dim3(256), x3::lds_bytes_pipe(), s, packed, X, M, ret,
-                           value, act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d);
-    } else if (waves == 4 && nt == 2) {
+    if (waves == 4 && nt == 2) {
       if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 4, 2);
       else X3_LAUNCH(K_CONT, 4, 2);
     } else if (waves == 4) {
