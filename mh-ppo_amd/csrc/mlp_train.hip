@@ -688,19 +688,13 @@ constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_
 constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
 constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
-constexpr int H_PART = 16 * IM_ROWB;  // half image (16 rows) of dW3's A operand, two-wave kernel
-constexpr int IMG_AL = (IMG + 15) / 16 * 16;
-// Per-wave slot of a kernel that interleaves NT tiles: NT images, 2 x NT input slots (double
-// buffered), the float64 loss sums, and (two-wave kernel) the half image H.
-template <int NT>
-struct WL {
-  static constexpr int O_IN = NT * IMG_AL, O_DACC = O_IN + 2 * NT * LY::IN_SZ * 4, O_H = O_DACC + 96 * 8,
-                       WAVE_B = O_H + (NT == 1 ? 3 * H_PART : 0);
-  static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
-};
-template <int WAVES, int NT>
-constexpr int lds_bytes() { return O_WAVE + WAVES * WL<NT>::WAVE_B; }
-static_assert(lds_bytes<8, 1>() <= 160 * 1024 && lds_bytes<4, 2>() <= 160 * 1024, "LDS budget");
+constexpr int WAVES = 4;  // one wave per SIMD
+// per-wave slot: the tile image (also the f32 transpose image), two input slots (double
+// buffered), the float64 loss sums
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_DACC + 96 * 8;
+constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
 
 #ifdef MHPPO_X3_PHASE
 __device__ __forceinline__ void x3_phase() { __builtin_amdgcn_sched_barrier(0); }
@@ -775,29 +769,17 @@ __device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
 // between the register files and the arch VGPRs stay free for the tile's values.  Written as
 // one asm block: "s_nop 1" covers the VALU-write -> MFMA-read hazard on A / B (the compiler
 // cannot see the MFMAs inside), and back-to-back accumulation into the same AGPRs needs none.
-// (two waves per SIMD share 256 registers: an AGPR-pinned accumulator would fix the split at
-// 128 + 128, so that kernel keeps the compiler's MFMAs: AG = false)
 #define X3_MACC6(OP)                                                                                 \
   asm("s_nop 1\n\t" OP " %0, %3, %4, %0\n\t" OP " %0, %1, %6, %0\n\t" OP " %0, %2, %5, %0\n\t" OP  \
       " %0, %2, %4, %0\n\t" OP " %0, %1, %5, %0\n\t" OP " %0, %1, %4, %0"                              \
       : "+a"(c)                                                                                      \
       : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2]))
-template <bool AG>
-__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) {
-  if constexpr (AG) X3_MACC6("v_mfma_f32_32x32x16_bf16");
-  else c = mfma6(a, b, c);
-}
-template <bool AG>
-__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) {
-  if constexpr (AG) X3_MACC6("v_mfma_f32_16x16x32_bf16");
-  else c = mfma6_16(a, b, c);
-}
+__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6("v_mfma_f32_32x32x16_bf16"); }
+__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6("v_mfma_f32_16x16x32_bf16"); }
 #undef X3_MACC6
 // before the accumulators are read: the last MFMA's result latency (>= 18 passes)
-template <bool AG>
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
-  if constexpr (AG)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
 }
 __device__ __forceinline__ uint2 lds_u2(const char *p) { return *reinterpret_cast<const uint2 *>(p); }
 __device__ __forceinline__ uint2 tr16(const char *p) {
@@ -893,13 +875,6 @@ __device__ __forceinline__ void stage_w(char *Wimg, int part, int rowb, int row,
   *reinterpret_cast<__bf16 *>(Wimg + part + off) = mid;
   *reinterpret_cast<__bf16 *>(Wimg + 2 * part + off) = lo;
 }
-// Hide a tile's values from common-subexpression elimination: the compiler would otherwise
-// keep a forward-pass split (1.5x the registers of the f32 tile) alive until the identical
-// split for the backward image, instead of the f32 tile it needs anyway for the ReLU masks.
-__device__ __forceinline__ void opaque(f32x16 &v) {
-#pragma unroll
-  for (int r = 0; r < 16; r++) asm volatile("" : "+v"(v[r]));
-}
 // d = (h > 0) ? d : 0 (ReLU derivative)
 __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 #pragma unroll
@@ -907,19 +882,18 @@ __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 }
 }  // namespace x3
 
-// WAVES = 8: two waves per SIMD (256 registers each); 4: one wave per SIMD (512 registers).
-// NT = tiles per loop iteration and wave (4 waves only): NT independent 32-row tiles go
-// through every phase side by side, so one in-order instruction stream carries two
-// dependency chains — the split arithmetic of one tile issues beside the MFMAs of the other.
-template <int KIND, int WAVES, int NT>
-__global__ void __launch_bounds__(64 * WAVES)
+// One wave per SIMD (4 waves per block, 512 registers: the weight-gradient accumulators and
+// the loop-invariant weight fragments sit in AGPRs).  Measured alternatives: two
+// waves per SIMD (256 registers force address rebuilds and recomputation: +40 % instructions,
+// no faster), two tiles per wave in lock step (spills), a software-pipelined loop (backward of
+// tile i beside the forward of tile i+1: 10 % slower).
+template <int KIND>
+__global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
                    float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
                    const double *__restrict__ stats, double m_global, float out_mean, float out_std,
                    float *__restrict__ gpart, double *__restrict__ dpart) {
   using namespace x3;
-  static_assert(NT == 1 || WAVES == 4, "tile interleave: one wave per SIMD");
-  using L = WL<NT>;
   extern __shared__ float lds[];
   char *L8 = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, l = tid & 63;
@@ -939,80 +913,46 @@ __global__ void __launch_bounds__(64 * WAVES)
   for (int i = tid; i < NF; i += 64 * WAVES)
     F[i] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
   __syncthreads();
-  char *wb = L8 + O_WAVE + w * L::WAVE_B;  // tile u's image / f32 transpose slot: wb + u * IMG_AL
-  float *inb = reinterpret_cast<float *>(wb + L::O_IN);
+  char *wb = L8 + O_WAVE + w * WAVE_B;  // this wave's image / f32 transpose slot
+  float *T = reinterpret_cast<float *>(wb);
+  float *inb = reinterpret_cast<float *>(wb + O_IN);
   const int j = l & 31, kh = l >> 5;
   const int G = l >> 4, q4 = (l >> 2) & 3, p4 = l & 3;
-  // Lane address bases: every fragment access is base + a constant.  With two waves per SIMD
-  // (256 registers) the bases are not held through the loop but rebuilt where used from a lane
-  // id the compiler cannot hoist (LN): a few VALU per use instead of ~20 loop-long registers.
-  auto LN = [&]() {
-    int v = l;
-    if constexpr (WAVES == 8) asm volatile("" : "+v"(v));
-    return v;
-  };
-  auto tr_off = [](int li, int rowb) {  // ds_read_b64_tr_b16 lane (4q + p of group G), 32x32x16 A/B
-    return (4 * ((li >> 5)) + ((li >> 2) & 3)) * rowb + 8 * (4 * ((li >> 4) & 1) + (li & 3));
-  };
-  auto w1row = [&]() { const int li = LN(); return (const char *)(L8 + O_W1 + (li & 31) * W1_ROWB + 16 * (li >> 5)); };
-  auto w2row = [&]() { const int li = LN(); return (const char *)(L8 + O_W2 + (li & 31) * W2_ROWB + 8 * (li >> 5)); };
-  auto w3row = [&]() { const int li = LN(); return (const char *)(L8 + O_W3 + (li & 31) * W3_ROWB + 8 * (li >> 5)); };
-  auto w2tr = [&]() { return (const char *)(L8 + O_W2 + tr_off(LN(), W2_ROWB)); };
-  auto w3tr = [&]() { return (const char *)(L8 + O_W3 + tr_off(LN(), W3_ROWB)); };
-  auto imw = [&](int u) { const int li = LN(); return wb + u * IMG_AL + (li & 31) * IM_ROWB + 8 * (li >> 5); };
-  // image reads: rows 8 (G >> 1) + 4u + q (tr_off with a doubled row step)
-  auto imr = [&](int u) {
-    const int li = LN();
-    return (const char *)(wb + u * IMG_AL + (8 * (li >> 5) + ((li >> 2) & 3)) * IM_ROWB +
-                          8 * (4 * ((li >> 4) & 1) + (li & 3)));
-  };
-  auto imr16 = [&](int u) {  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
-    const int li = LN();
-    return (const char *)(wb + u * IMG_AL + (8 * (li >> 4) + ((li >> 2) & 3)) * IM_ROWB + 8 * (li & 3));
-  };
-  auto Tu = [&](int u) { return reinterpret_cast<float *>(wb + u * IMG_AL); };
+  // lane address bases: every fragment access below is one of these plus a constant
+  const char *w1row = L8 + O_W1 + j * W1_ROWB + 16 * kh;
+  const char *w2row = L8 + O_W2 + j * W2_ROWB + 8 * kh;
+  const char *w3row = L8 + O_W3 + j * W3_ROWB + 8 * kh;
+  const char *w2tr = L8 + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
+  const char *w3tr = L8 + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
+  char *imw = wb + j * IM_ROWB + 8 * kh;
+  // image reads: rows 8 (G >> 1) + 4u + q, chunk 4 (G & 1) + p
+  const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
+  const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
   const float b40 = uniform_f(F[128]);
-  // One wave per SIMD (512 registers): the weight fragments are loop invariants, read from LDS
-  // once here instead of once per tile
-  // the forward ones too for the critic pass (the actor pass's loss needs those registers)
-  constexpr bool HF = WAVES == 4 && NT == 1 && KIND == K_CRITIC;
-#ifdef MHPPO_X3_NO_HOIST_BWD
-  constexpr bool HB = false;
-#else
-  constexpr bool HB = WAVES == 4;  // measured: -3 % (the forward ones as well spill kind 1)
-#endif
-  constexpr bool AG = WAVES == 4;  // weight-gradient accumulators pinned to AGPRs (macc6)
+  // Loop-invariant weight fragments read from LDS once: the backward W^T ones, and for the
+  // critic pass the forward ones too (the actor pass's loss needs those registers)
+  constexpr bool HF = KIND == K_CRITIC;
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
   if constexpr (HF) {
     for (int t = 0; t < 2; t++)
-      for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row(), t, s);
-    for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row(), 0, s);
+      for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
+    for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   }
-  if constexpr (HB) {
-    for (int t = 0; t < 2; t++)
-      for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr(), t, s);
-    for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr(), 0, s);
-  }
+  for (int t = 0; t < 2; t++)
+    for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
+  for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
   auto fw2 = [&](int t, int s) -> F3 {
     if constexpr (HF) return wf2[t][s];
-    else return w_fwd<W2_ROWB, W2_PART>(w2row(), t, s);
+    else return w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
   };
   auto fw3 = [&](int s) -> F3 {
     if constexpr (HF) return wf3[s];
-    else return w_fwd<W3_ROWB, W3_PART>(w3row(), 0, s);
-  };
-  auto bw3 = [&](int t, int s) -> F3 {
-    if constexpr (HB) return wb3[t][s];
-    else return w_bwd<W3_ROWB, W3_PART>(w3tr(), t, s);
-  };
-  auto bw2 = [&](int s) -> F3 {
-    if constexpr (HB) return wb2[s];
-    else return w_bwd<W2_ROWB, W2_PART>(w2tr(), 0, s);
+    else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   };
   f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
   f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float gB2a = 0.f, gB2b = 0.f, gB3 = 0.f, gW4 = 0.f, gB4 = 0.f;
-  double *dacc = reinterpret_cast<double *>(wb + L::O_DACC) + j;
+  double *dacc = reinterpret_cast<double *>(wb + O_DACC) + j;
   if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
   float meanf = 0.f, stdf = 1.f;
   if (KIND != K_CRITIC) {
@@ -1023,284 +963,198 @@ __global__ void __launch_bounds__(64 * WAVES)
   }
   const double inv_m = uniform_d(1.0 / m_global);
   const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
-  const int64_t ngroups = (ntiles + NT - 1) / NT;  // tile group p = tiles NT p .. NT p + NT - 1
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  auto group_full = [&](int64_t p) { return p * NT + NT - 1 < nfull; };  // every tile of group p is full: DMA
 
   int cb = 0;
-  if (gw < ngroups && group_full(gw)) {
-#pragma unroll
-    for (int u = 0; u < NT; u++) prefetch_tile<KIND, LY>(inb + u * LY::IN_SZ, X, ret, V, act, lp_old, (gw * NT + u) * 32, l);
-  }
-  for (int64_t grp = gw; grp < ngroups; grp += nw, cb ^= 1) {
-    int64_t row0[NT];
-    int nrows[NT];
-    float *slot[NT];
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      row0[u] = (grp * NT + u) * 32;
-      nrows[u] = (int)max((int64_t)0, min((int64_t)32, M - row0[u]));
-      slot[u] = inb + (cb * NT + u) * LY::IN_SZ;
-    }
-    const int64_t nxt = grp + nw;
-    if (nxt < ngroups && group_full(nxt)) {
-#pragma unroll
-      for (int u = 0; u < NT; u++)
-        prefetch_tile<KIND, LY>(inb + ((cb ^ 1) * NT + u) * LY::IN_SZ, X, ret, V, act, lp_old, (nxt * NT + u) * 32, l);
-      wait_vmcnt<NT * prefetch_ops<KIND>()>();
-    } else if (group_full(grp)) {
+  if (gw < nfull) prefetch_tile<KIND, LY>(inb, X, ret, V, act, lp_old, gw * 32, l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
+    const int64_t row0 = tile * 32;
+    const int nrows = (int)min((int64_t)32, M - row0);
+    float *slot = inb + cb * LY::IN_SZ;
+    const int64_t nxt = tile + nw;
+    if (nxt < nfull) {
+      prefetch_tile<KIND, LY>(inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
+      wait_vmcnt<prefetch_ops<KIND>()>();
+    } else if (tile < nfull) {
       wait_vmcnt<0>();
+    } else {
+      load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
     }
-    if (!group_full(grp)) {  // the ragged end: plain loads, rows past M (and tiles past the last) read 0
-#pragma unroll
-      for (int u = 0; u < NT; u++) load_tile_sync<KIND, LY>(slot[u], X, nin, ret, V, act, lp_old, row0[u], nrows[u], l);
-    }
-    wave_sync();  // the tiles' inputs have landed
+    wave_sync();  // the tile's inputs have landed
+    const float *Xs = slot + LY::IN_X;
     // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
-    auto layer1 = [&](int u) {
-      const float *Xs = slot[u] + LY::IN_X;
+    f32x16 h1;
+    {
       float v8[8];
-      const int li = LN();
 #pragma unroll
       for (int q = 0; q < 8; q++) {
         // row j, input column k = 8h + q (h = 1: columns 8..15; 13 is the bias input).  Columns
         // 13-15 read the next row's first inputs (the slot's last row reads into its s0 block).
-        const int k = 8 * (li >> 5) + q;
-        const float v = Xs[(li & 31) * nin + 8 * (li >> 5) + q];
+        const int k = 8 * kh + q;
+        const float v = Xs[j * nin + 8 * kh + q];
         v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
       }
-      f32x16 h = mfma6(rd_pair<W1_PART>(w1row(), 8), split8(v8), zero16());
-      relu16(h);
-      return h;
-    };
-    f32x16 h1[NT], h2a[NT], h2b[NT], h3[NT], d3[NT], d2a[NT], d2b[NT], d1[NT];
-    F3 d3f0[NT], d3f1[NT];
-    float dy0[NT];
-#pragma unroll
-    for (int u = 0; u < NT; u++) h1[u] = layer1(u);
-    x3_phase();
-    // ---- layer 2
-    // the biases ride in as the chains' initial accumulators (no VALU adds, no LDS wait in the
-    // middle of the layer)
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      h2a[u] = feat_vec(F, LN() >> 5);
-      h2b[u] = feat_vec(F + 32, LN() >> 5);
-#pragma unroll
-      for (int s = 0; s < 2; s++) {
-        const F3 b = split_step(h1[u], s);
-        h2a[u] = mfma6(fw2(0, s), b, h2a[u]);
-        h2b[u] = mfma6(fw2(1, s), b, h2b[u]);
-      }
-      relu16(h2a[u]);
-      relu16(h2b[u]);
+      h1 = mfma6(rd_pair<W1_PART>(w1row, 8), split8(v8), zero16());
+      relu16(h1);
     }
+    x3_phase();
+    // ---- layer 2 (the biases ride in as the chains' initial accumulators)
+    f32x16 h2a = feat_vec(F, kh), h2b = feat_vec(F + 32, kh);
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const F3 b = split_step(h1, s);
+      h2a = mfma6(fw2(0, s), b, h2a);
+      h2b = mfma6(fw2(1, s), b, h2b);
+    }
+    relu16(h2a);
+    relu16(h2b);
     x3_phase();
     // ---- layer 3
+    f32x16 h3 = feat_vec(F + 64, kh);
 #pragma unroll
-    for (int u = 0; u < NT; u++) {
-      h3[u] = feat_vec(F + 64, LN() >> 5);
+    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(s), split_step(h2a, s), h3);
 #pragma unroll
-      for (int s = 0; s < 2; s++) h3[u] = mfma6(fw3(s), split_step(h2a[u], s), h3[u]);
-#pragma unroll
-      for (int s = 0; s < 2; s++) h3[u] = mfma6(fw3(2 + s), split_step(h2b[u], s), h3[u]);
-      relu16(h3[u]);
-    }
+    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(2 + s), split_step(h2b, s), h3);
+    relu16(h3);
     x3_phase();
-    // ---- loss gradient dL/dy for this lane's row (as the f32 path)
+    // ---- output and loss gradient dL/dy for this lane's row (as the f32 path)
+    const f32x16 w4v = feat_vec(F + 96, kh);
+    float part0 = 0.0f;
 #pragma unroll
-    for (int u = 0; u < NT; u++) {
-      const f32x16 w4v = feat_vec(F + 96, LN() >> 5);
-      float part0 = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; r++) part0 = fmaf(w4v[r], h3[u][r], part0);
-      const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
-      const bool valid = j < nrows[u];
-      const float *sl = slot[u];
-      dy0[u] = 0.0f;
-      if (valid) {
-        const float rt = sl[LY::IN_S0 + j];
-        if constexpr (KIND == K_CRITIC) {
-          const float v = y0;
-          if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0[u], 128), 4 * j, 0, 0);
-          const float a = rt - v;
-          const float d = v - rt;
-          if (kh == 0) {
-            dacc[0] += (double)d * (double)d;
-            dacc[32] += (double)a;
-            dacc[64] += (double)a * (double)a;
-          }
-          dy0[u] = (float)(2.0 * inv_m * (double)d);
-        } else {
-          const float t = tanhf(y0);
-          const float mu = t * out_std + out_mean;
-          const float a = rt - sl[LY::IN_S0 + 32 + j];
-          const float A = (a - meanf) / (stdf + 1e-10f);
-          const float diff = (float)((double)sl[LY::IN_S1 + j] - (double)mu);
-          const float x = diff * MVN_INV_L;
-          const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-          const double r = exp((double)lp - (double)sl[LY::IN_S1 + 32 + j]);
-          double dfdr;
-          const double f = surr_and_grad(r, (double)A, dfdr);
-          if (kh == 0) dacc[0] += f;
-          const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
-          dy0[u] = (dmu * out_std) * (1.0f - t * t);
+    for (int r = 0; r < 16; r++) part0 = fmaf(w4v[r], h3[r], part0);
+    const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
+    const bool valid = j < nrows;
+    float dy0 = 0.0f;
+    if (valid) {
+      const float rt = slot[LY::IN_S0 + j];
+      if constexpr (KIND == K_CRITIC) {
+        const float v = y0;
+        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
+        const float a = rt - v;
+        const float d = v - rt;
+        if (kh == 0) {
+          dacc[0] += (double)d * (double)d;
+          dacc[32] += (double)a;
+          dacc[64] += (double)a * (double)a;
         }
+        dy0 = (float)(2.0 * inv_m * (double)d);
+      } else {
+        const float t = tanhf(y0);
+        const float mu = t * out_std + out_mean;
+        const float a = rt - slot[LY::IN_S0 + 32 + j];
+        const float A = (a - meanf) / (stdf + 1e-10f);
+        const float diff = (float)((double)slot[LY::IN_S1 + j] - (double)mu);
+        const float x = diff * MVN_INV_L;
+        const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
+        const double r = exp((double)lp - (double)slot[LY::IN_S1 + 32 + j]);
+        double dfdr;
+        const double f = surr_and_grad(r, (double)A, dfdr);
+        if (kh == 0) dacc[0] += f;
+        const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+        dy0 = (dmu * out_std) * (1.0f - t * t);
       }
-      gB4 += (kh == 0) ? dy0[u] : 0.0f;
-      // layer 4 backward: d3 = dH3^T masked (w4 as loaded for the output)
-#pragma unroll
-      for (int r = 0; r < 16; r++) d3[u][r] = (h3[u][r] > 0.0f) ? w4v[r] * dy0[u] : 0.0f;
     }
-    // ---- dW4 = row sums of dy h3; dB3 = row sums of d3
+    gB4 += (kh == 0) ? dy0 : 0.0f;
+    // ---- layer 4 backward: d3 = dH3^T masked; dW4 = row sums of dy h3; dB3 = row sums of d3
+    f32x16 g, d3;
 #pragma unroll
-    for (int u = 0; u < NT; u++) {
-      f32x16 g;
-#pragma unroll
-      for (int r = 0; r < 16; r++) g[r] = dy0[u] * h3[u][r];
-      float *T = Tu(u);
-      put_t(T, g, LN());
-      lds_order();
-      gW4 += half_row_sum(T, LN());
-      lds_order();
-      put_t(T, d3[u], LN());
-      lds_order();
-      gB3 += half_row_sum(T, LN());
-      lds_order();
+    for (int r = 0; r < 16; r++) {
+      g[r] = dy0 * h3[r];
+      d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
     }
+    put_t(T, g, l);
+    lds_order();
+    gW4 += half_row_sum(T, l);
+    lds_order();
+    put_t(T, d3, l);
+    lds_order();
+    gB3 += half_row_sum(T, l);
+    lds_order();
     x3_phase();
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      d3f0[u] = split_step(d3[u], 0);
-      d3f1[u] = split_step(d3[u], 1);
-    }
-    if constexpr (WAVES == 8) {
-      opaque(h2a[0]);
-      opaque(h2b[0]);
-      // registers: one K-step of the A operand at a time, staged through the half image H
-      // (rows 16s..16s+15 of d3, written by the lanes holding those rows) while the slot holds
-      // the B image: h2a (s = 0, 1), then h2b (s = 1 with the A fragment kept, then s = 0)
-      auto d3_half = [&](int s) {
-        if ((j >> 4) == s) img_write<H_PART>(imw(0) + L::O_H - 16 * IM_ROWB * s, d3f0[0], d3f1[0]);
-        lds_order();
-        const F3 a = tr_pair<H_PART>(imr(0) + L::O_H, 4 * IM_ROWB);
-        lds_order();
-        return a;
-      };
-      img_write(imw(0), split_step(h2a[0], 0), split_step(h2a[0], 1));
-      lds_order();
-      F3 ad = d3_half(0);
-      macc6<AG>(ad, img_read(imr(0), 0), gW3a);
-      ad = d3_half(1);
-      macc6<AG>(ad, img_read(imr(0), 1), gW3a);
-      lds_order();
-      img_write(imw(0), split_step(h2b[0], 0), split_step(h2b[0], 1));
-      lds_order();
-      macc6<AG>(ad, img_read(imr(0), 1), gW3b);
-      ad = d3_half(0);
-      macc6<AG>(ad, img_read(imr(0), 0), gW3b);
-      lds_order();
-    } else {
-#pragma unroll
-      for (int u = 0; u < NT; u++) {
-        img_write(imw(u), d3f0[u], d3f1[u]);
-        lds_order();
-        const F3 ad0 = img_read(imr(u), 0), ad1 = img_read(imr(u), 1);
-        lds_order();
-        img_write(imw(u), split_step(h2a[u], 0), split_step(h2a[u], 1));
-        lds_order();
-        macc6<AG>(ad0, img_read(imr(u), 0), gW3a);
-        macc6<AG>(ad1, img_read(imr(u), 1), gW3a);
-        lds_order();
-        img_write(imw(u), split_step(h2b[u], 0), split_step(h2b[u], 1));
-        lds_order();
-        macc6<AG>(ad0, img_read(imr(u), 0), gW3b);
-        macc6<AG>(ad1, img_read(imr(u), 1), gW3b);
-        lds_order();
-      }
-    }
+    const F3 d3f0 = split_step(d3, 0), d3f1 = split_step(d3, 1);
+    img_write(imw, d3f0, d3f1);
+    lds_order();
+    const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
+    lds_order();
+    img_write(imw, split_step(h2a, 0), split_step(h2a, 1));
+    lds_order();
+    macc6(ad0, img_read(imr, 0), gW3a);
+    macc6(ad1, img_read(imr, 1), gW3a);
+    lds_order();
+    img_write(imw, split_step(h2b, 0), split_step(h2b, 1));
+    lds_order();
+    macc6(ad0, img_read(imr, 0), gW3b);
+    macc6(ad1, img_read(imr, 1), gW3b);
+    lds_order();
     x3_phase();
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      d2a[u] = zero16();
-      d2b[u] = zero16();
-      d2a[u] = mfma6(bw3(0, 0), d3f0[u], d2a[u]);
-      d2a[u] = mfma6(bw3(0, 1), d3f1[u], d2a[u]);
-      d2b[u] = mfma6(bw3(1, 0), d3f0[u], d2b[u]);
-      d2b[u] = mfma6(bw3(1, 1), d3f1[u], d2b[u]);
-      relu_mask(d2a[u], h2a[u]);
-      relu_mask(d2b[u], h2b[u]);
-      float *T = Tu(u);
-      put_t(T, d2a[u], LN());
-      lds_order();
-      gB2a += half_row_sum(T, LN());
-      lds_order();
-      put_t(T, d2b[u], LN());
-      lds_order();
-      gB2b += half_row_sum(T, LN());
-      lds_order();
-    }
+    f32x16 d2a = zero16(), d2b = zero16();
+    d2a = mfma6(wb3[0][0], d3f0, d2a);
+    d2a = mfma6(wb3[0][1], d3f1, d2a);
+    d2b = mfma6(wb3[1][0], d3f0, d2b);
+    d2b = mfma6(wb3[1][1], d3f1, d2b);
+    relu_mask(d2a, h2a);
+    relu_mask(d2b, h2b);
+    put_t(T, d2a, l);
+    lds_order();
+    gB2a += half_row_sum(T, l);
+    lds_order();
+    put_t(T, d2b, l);
+    lds_order();
+    gB2b += half_row_sum(T, l);
+    lds_order();
     x3_phase();
-    // two waves per SIMD: h1 is recomputed here rather than held through layers 2-3 (registers)
-    if constexpr (WAVES == 8) {
-      lds_order();
-      h1[0] = layer1(0);
-    }
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      d1[u] = zero16();
-      const F3 f0 = split_step(d2a[u], 0), f1 = split_step(d2a[u], 1);
-      d1[u] = mfma6(bw2(0), f0, d1[u]);
-      d1[u] = mfma6(bw2(1), f1, d1[u]);
+    f32x16 d1 = zero16();
+    {
+      const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
+      d1 = mfma6(wb2[0], f0, d1);
+      d1 = mfma6(wb2[1], f1, d1);
       // B = h1 image, A = d2a image
-      img_write(imw(u), split_step(h1[u], 0), split_step(h1[u], 1));
+      img_write(imw, split_step(h1, 0), split_step(h1, 1));
       lds_order();
-      const F3 bh0 = img_read(imr(u), 0), bh1 = img_read(imr(u), 1);
+      const F3 bh0 = img_read(imr, 0), bh1 = img_read(imr, 1);
       lds_order();
-      img_write(imw(u), f0, f1);
+      img_write(imw, f0, f1);
       lds_order();
-      macc6<AG>(img_read(imr(u), 0), bh0, gW2a);
-      macc6<AG>(img_read(imr(u), 1), bh1, gW2a);
+      macc6(img_read(imr, 0), bh0, gW2a);
+      macc6(img_read(imr, 1), bh1, gW2a);
       lds_order();
-      const F3 f2 = split_step(d2b[u], 0), f3 = split_step(d2b[u], 1);
-      d1[u] = mfma6(bw2(2), f2, d1[u]);
-      d1[u] = mfma6(bw2(3), f3, d1[u]);
-      img_write(imw(u), f2, f3);
+      const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
+      d1 = mfma6(wb2[2], f2, d1);
+      d1 = mfma6(wb2[3], f3, d1);
+      img_write(imw, f2, f3);
       lds_order();
-      macc6<AG>(img_read(imr(u), 0), bh0, gW2b);
-      macc6<AG>(img_read(imr(u), 1), bh1, gW2b);
+      macc6(img_read(imr, 0), bh0, gW2b);
+      macc6(img_read(imr, 1), bh1, gW2b);
       lds_order();
-      relu_mask(d1[u], h1[u]);
     }
+    relu_mask(d1, h1);
     x3_phase();
     // ---- dW1 = sum over rows of d1 (x) [X | 1]: A = d1 image, B = the input rows (column 13:
     // the constant 1, i.e. dB1).  16x16x32 tiles (out features 16t..16t+15 x input columns
     // 0..15, all 32 rows in one K-step): lane l of group G = l >> 4 holds rows 8G..8G+7 of
     // column l & 15 / feature l & 15
-#pragma unroll
-    for (int u = 0; u < NT; u++) {
-      img_write(imw(u), split_step(d1[u], 0), split_step(d1[u], 1));
-      lds_order();
-      const float *Xs = slot[u] + LY::IN_X;
+    img_write(imw, split_step(d1, 0), split_step(d1, 1));
+    lds_order();
+    {
       float xv[8];
-      const int li = LN(), n = li & 15;
+      const int n = l & 15;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
-        const float v = Xs[(8 * (li >> 4) + q) * nin + (n < nin ? n : 0)];
+        const float v = Xs[(8 * G + q) * nin + (n < nin ? n : 0)];
         xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
       }
       const F3 b = split8(xv);
-      macc6_16<AG>(tr_pair<IM_PART>(imr16(u), 4 * IM_ROWB), b, gW1t[0]);
-      macc6_16<AG>(tr_pair<IM_PART>(imr16(u) + 32, 4 * IM_ROWB), b, gW1t[1]);
-      lds_order();
+      macc6_16(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
+      macc6_16(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
     }
+    lds_order();
     x3_phase();
   }
   // ---- write this wave's partial gradient (packed torch layout)
-  macc_drain<AG>(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
+  macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
   float *gp = gpart + (size_t)gw * NWP;
 #pragma unroll
   for (int r = 0; r < 16; r++) {
@@ -1402,26 +1256,6 @@ void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int n
 }
 }  // namespace
 
-// waves per block of the split-precision kernel: 8 (two per SIMD) or 4 (one per SIMD, 512
-// registers); MHPPO_X3_WAVES overrides for A/B runs
-int x3_waves() {
-  static int w = 0;
-  if (!w) {
-    const char *e = getenv("MHPPO_X3_WAVES");
-    w = (e && atoi(e) == 8) ? 8 : 4;  // 8 (two waves per SIMD) once its loop fits 256 registers
-  }
-  return w;
-}
-// tiles interleaved per wave in lock step (one wave per SIMD only; A/B runs): MHPPO_X3_NT=2
-int x3_nt() {
-  static int n = 0;
-  if (!n) {
-    const char *e = getenv("MHPPO_X3_NT");
-    n = (e && atoi(e) == 2) ? 2 : 1;
-  }
-  return n;
-}
-
 #ifdef MHPPO_TIMING
 // A/B timing builds only (not in include/mhppo.h): copy out and clear this TU's g_timing
 extern "C" int mhppo_debug_timing_train(unsigned long long *out16) {
@@ -1464,11 +1298,10 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     wk.cus = cus;
   }
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
-  const int waves = split ? x3_waves() : (pf ? 8 : 4);
-  const int nt = split && waves == 4 ? x3_nt() : 1;  // tiles per wave and loop iteration
-  int64_t blocks = wk.cus;  // one block per CU, grid-stride over groups of nt 32-row tiles
-  const int64_t groups = ((M + 31) / 32 + nt - 1) / nt;
-  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (groups + waves - 1) / waves));
+  const int waves = split ? x3::WAVES : (pf ? 8 : 4);
+  int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
+  const int64_t tiles = (M + 31) / 32;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
   const int nw = (int)blocks * waves;
   if (wk.nw < nw) {
     if (wk.g) (void)hipFree(wk.g);
@@ -1485,19 +1318,11 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   const dim3 grid((unsigned)blocks);
 #define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
   if (split) {
-#define X3_LAUNCH(KIND_, W_, NT_)                                                                         \
-  hipLaunchKernelGGL((k_mlp_train_x3<KIND_, W_, NT_>), grid, dim3(64 * W_), (x3::lds_bytes<W_, NT_>()), s, packed, \
-                     X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
-    if (waves == 4 && nt == 2) {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 4, 2);
-      else X3_LAUNCH(K_CONT, 4, 2);
-    } else if (waves == 4) {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 4, 1);
-      else X3_LAUNCH(K_CONT, 4, 1);
-    } else {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 8, 1);
-      else X3_LAUNCH(K_CONT, 8, 1);
-    }
+#define X3_LAUNCH(KIND_)                                                                                    \
+  hipLaunchKernelGGL((k_mlp_train_x3<KIND_>), grid, dim3(64 * x3::WAVES), x3::LDS_BYTES, s, packed, X, M, ret, value, \
+                     act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
+    if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC);
+    else X3_LAUNCH(K_CONT);
 #undef X3_LAUNCH
   } else if (pf) {
     if (kind == K_CRITIC)

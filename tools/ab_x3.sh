@@ -1,13 +1,12 @@
 #!/bin/bash
-# A/B of the split-precision train kernel: build variants x waves, plus the exact f32 kernel
-# usage: bash tools/ab_x3.sh <variant>... (base = the in-tree library, else build_ab/<v>/libmhppo.so)
+# A/B of the split-precision train kernel across library builds, plus the exact f32 kernel:
+# usage: bash tools/ab_x3.sh <variant>... (base = the in-tree library, else build_ab/<v>/libmhppo.so,
+# built by tools/ab_build.sh <v> "<flags>")
 set -o pipefail
 for v in "$@"; do
   if [ "$v" = base ]; then lib=""; else lib="build_ab/$v/libmhppo.so"; fi
-  for w in ${WAVES:-4 8}; do
-    echo "== $v waves=$w"
-    MHPPO_X3_WAVES=$w MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 || exit 1
-  done
+  echo "== $v split"
+  MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 || exit 1
   echo "== $v exact f32"
   MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 --exact || exit 1
 done
