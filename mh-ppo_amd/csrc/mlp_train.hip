@@ -705,9 +705,10 @@ __device__ __forceinline__ void x3_phase() {}
 // so only the compiler must keep the write -> read order (no lgkmcnt drain)
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
-__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
-  bf16x2 v = {(__bf16)x, (__bf16)y};
-  return __builtin_bit_cast(uint32_t, v);
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {  // one v_cvt_pk_bf16_f32
+  const f32x2 v = {x, y};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 // (x, y) -> three packed bf16 pairs, x = hi + mid + lo exactly (element 0 in the low half)
 __device__ __forceinline__ void split_pair(float x, float y, uint32_t &h, uint32_t &m, uint32_t &lo) {
