@@ -127,18 +127,27 @@ MHPPO_HD int write_car_obs(const EV &E, int s, float *o) {
 
 // flat obs (gym-sorted car|car_follow|env|ped); ped.get_data runs even without
 // an obs buffer because it advances the running-min `delta` (:441).
+// The register view (EV::OBS_DIM > 0) builds the row in its staging buffer (the wave's LDS
+// image on the device) and writes the wave's 64 rows as one coalesced block
+// (EnvR::store_obs_row); the generic view writes the row in place.
 template <class EV>
 MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
   constexpr int V = EV::VAR;
+  constexpr int OD = EV::OBS_DIM;
   const Cfg &c = E.c;
-  float *o = obs ? obs + (size_t)E.e * c.obs_dim : nullptr;
+  float *o;
+  if constexpr (OD > 0) o = E.obs_stage();
+  else o = obs ? obs + (size_t)E.e * c.obs_dim : nullptr;
   float tmp[8];
   int k = 0;
   if (o) {
     MHPPO_UNROLL
     for (int s = 0; s < E.nC(); s++) {
-      int w = write_car_obs(E, s, tmp);
-      for (int j = 0; j < w; j++) o[k++] = tmp[j];
+      const int w = write_car_obs(E, s, tmp);
+      MHPPO_UNROLL
+      for (int j = 0; j < 8; j++)  // w <= 7, known after inlining: constant offsets
+        if (j < w) o[k + j] = tmp[j];
+      k += w;
     }
     o[k++] = (float)(E.cross * (double)c.nb_lines / 2.);
     o[k++] = (float)E.ped_traffic();
@@ -151,8 +160,16 @@ MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
     double d[9];
     ped_get_data(E, q, mode, d);
     E.pedf(P_DELTA, p) = q.delta;
-    if (o)
-      for (int j = 0; j < 9; j++) o[k++] = (float)d[j];
+    if (o) {
+      MHPPO_UNROLL
+      for (int j = 0; j < 9; j++) o[k + j] = (float)d[j];
+      k += 9;
+    }
+  }
+  if constexpr (OD > 0) {
+#ifndef MHPPO_EXP_NO_OBS
+    if (obs) E.store_obs_row(obs);
+#endif
   }
 }
 
@@ -319,6 +336,9 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
       car_step(E, nS + i, a, light);
     }
   }
+#ifndef MHPPO_EXP_NO_COMMIT
+  E.commit_cars();
+#endif
   MHPPO_MARK(4);
   MHPPO_UNROLL
   for (int p = 0; p < E.nP(); p++) {
@@ -326,6 +346,9 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     ped_step(E, q, time);
     store_ped(E, p, q, true);
   }
+#ifndef MHPPO_EXP_NO_COMMIT
+  E.commit_peds();
+#endif
   MHPPO_MARK(5);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) acc[i] = 0.;
@@ -336,6 +359,9 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     ped_detection(E, q, prev, acc, add);
     E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
   }
+#ifndef MHPPO_EXP_NO_COMMIT
+  E.commit_det();
+#endif
   MHPPO_MARK(6);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {

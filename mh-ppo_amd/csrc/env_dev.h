@@ -138,6 +138,29 @@ MHPPO_HD __forceinline__ size_t npad(int N) { return ((size_t)N + EB - 1) / EB *
 MHPPO_HD __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
 MHPPO_HD __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
 
+// x**2 and x**4 (CPython float_pow -> glibc pow, <= 0.52 ulp, i.e. the correctly rounded
+// power but for rare near-midpoint cases).  The device computes the correctly rounded square
+// and a double-double fourth power (one rounding) instead of ocml's general pow (~130
+// instructions through an extended-precision log/exp); the host build (tools/hostsim.cpp)
+// keeps glibc's pow, so the simulator stays bit-identical to the oracle.
+MHPPO_HD __forceinline__ double pow_2(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return x * x;
+#else
+  return pow(x, 2.0);
+#endif
+}
+MHPPO_HD __forceinline__ double pow_4(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const double x2 = x * x, r = x2 * x2;
+  if (!(fabs(r) < 0x1p1000) || fabs(x2) < 0x1p-400) return r;  // inf/NaN/overflow, tiny: plain
+  const double e = fma(x, x, -x2);                                // x^2 == x2 + e exactly
+  return fma(x2, x2, 2.0 * x2 * e);  // x2^2 + 2 x2 e (+ e^2 < 2^-106 x^4), rounded once
+#else
+  return pow(x, 4.0);
+#endif
+}
+
 static constexpr double PI = 0x1.921fb54442d18p+1;
 static constexpr double NV_MAGICCONST = 0x1.b72cd3f331398p+0;  // 4*exp(-0.5)/sqrt(2.0)
 
@@ -321,6 +344,9 @@ struct Env {
     b.envi[sidx(EI_NI, EI_MTI, e)] = rng.mti;
     b.envi[sidx(EI_NI, EI_MTB, e)] = rng.mtb;
   }
+  MHPPO_HD void commit_cars() {}  // in place: nothing staged
+  MHPPO_HD void commit_peds() {}
+  MHPPO_HD void commit_det() {}
   MHPPO_HD void commit() { save_rng(); }
   MHPPO_HD int nC() const { return c.nC; }
   MHPPO_HD int nAV() const { return c.nAV; }
@@ -334,6 +360,44 @@ struct Env {
   MHPPO_HD double &pedf(int f, int p) const { return b.ped[sidx(P_NF * c.P, f * c.P + p, e)]; }
   MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[sidx(c.P, p, e)]; }
 };
+
+#ifdef __HIP__
+// One observation row per lane, obs [N][OD] f32: the wave's 64 rows are one contiguous
+// 256*OD-byte block, but row-per-lane stores put each instruction's 64 lanes 4*OD bytes
+// apart (64 partial cache lines per instruction, OD instructions).  The register view
+// builds its row straight into this wave's LDS image of the block ([64][OD], the block's
+// exact memory image; obs_lds_row), and store_obs_wave writes the block out as
+// lane-contiguous 16-B stores: OD/4 fully coalesced instructions.  Every lane of a full
+// wave must call it (convergent); a partial wave (or a misaligned caller buffer) copies its
+// rows out one per lane.  Workgroups of 4 waves (TPB = 256 in every register-view kernel).
+template <int OD>
+__device__ __forceinline__ float *obs_lds_wave() {
+  __shared__ float sh_obs[4][64 * OD];
+  return sh_obs[(threadIdx.x >> 6) & 3];
+}
+template <int OD>
+__device__ __forceinline__ float *obs_lds_row() { return obs_lds_wave<OD>() + (threadIdx.x & 63) * OD; }
+template <int OD>
+__device__ __forceinline__ void store_obs_wave(float *obs, int e, int N) {
+  const int lane = threadIdx.x & 63;
+  const int e0 = e - lane;
+  const float *s = obs_lds_wave<OD>();
+  float *wbase = obs + (size_t)e0 * OD;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (e0 + 64 > N || ((uintptr_t)wbase & 15) != 0) {
+#pragma unroll
+    for (int k = 0; k < OD; k++) obs[(size_t)e * OD + k] = s[lane * OD + k];
+    return;
+  }
+  constexpr int NCH = 16 * OD;  // 16-B chunks of the wave's block
+  const float4 *src = reinterpret_cast<const float4 *>(s);
+  float4 *dst = reinterpret_cast<float4 *>(wbase);
+#pragma unroll
+  for (int q = lane; q < NCH; q += 64) dst[q] = src[q];
+}
+#endif
 
 // EnvR<V, NC, NAV, NP>: compile-time shape (NC car slots, NAV AVs, NP pedestrians).
 // The whole env state is loaded into registers in one batch of independent loads at
@@ -384,31 +448,57 @@ struct EnvR {
     // the RNG window is fetched at the start of the step (env_step_body): its address
     // depends on the cursor loaded here, and the car steps cover the round trip
   }
-  // dynamic fields only: line/exist and the pedestrian's static draws never change in a step
-  MHPPO_HD void commit() {
-    const size_t N = (size_t)c.N;
+  // Dynamic fields only (line/exist and the pedestrian's static draws never change in a
+  // step), each group stored as soon as env_step_body is done with it, so the stores drain
+  // while the rest of the step computes instead of in one burst at the end: the cars'
+  // kinematics and history bits after the car steps (commit_cars), the pedestrians'
+  // kinematics and the RNG cursor after the pedestrian step (commit_peds; no later phase
+  // draws), the detection fields after detection (commit_det), the rest in commit().
+  MHPPO_HD void commit_cars() {
     constexpr int dyn_car[4] = {C_AC, C_VC, C_SC, C_LIGHT};
-    constexpr int det_car[3] = {C_PA, C_ES, C_TS};
-    constexpr int dyn_ped[10] = {P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_WDL, P_DELTA, P_LPOS};
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll
       for (int s = 0; s < NC; s++) b.car[sidx(C_NF * NC, dyn_car[k] * NC + s, e)] = car_[dyn_car[k]][s];
     b.envi[sidx(EI_NI, EI_H0NF, e)] = hnf_[0];
     b.envi[sidx(EI_NI, EI_H1NF, e)] = hnf_[1];
+  }
+  MHPPO_HD void commit_peds() {
+    constexpr int kin_ped[8] = {P_SX, P_SY, P_VX, P_VY, P_T0, P_WT, P_CT, P_LPOS};
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+      for (int p = 0; p < NP; p++) b.ped[sidx(P_NF * NP, kin_ped[k] * NP + p, e)] = ped_[kin_ped[k]][p];
+    b.envi[sidx(EI_NI, EI_MTI, e)] = rng.mti;
+    b.envi[sidx(EI_NI, EI_MTB, e)] = rng.mtb;
+  }
+  MHPPO_HD void commit_det() {
+    constexpr int det_car[3] = {C_PA, C_ES, C_TS};
 #pragma unroll
     for (int k = 0; k < 3; k++)
 #pragma unroll
       for (int s = 0; s < NAV; s++) b.car[sidx(C_NF * NC, det_car[k] * NC + s, e)] = car_[det_car[k]][s];
-#pragma unroll
-    for (int k = 0; k < 10; k++)
-#pragma unroll
-      for (int p = 0; p < NP; p++) b.ped[sidx(P_NF * NP, dyn_ped[k] * NP + p, e)] = ped_[dyn_ped[k]][p];
-#pragma unroll
-    for (int p = 0; p < NP; p++) b.pfl[sidx(NP, p, e)] = pfl_[p];
-    b.envi[sidx(EI_NI, EI_MTI, e)] = rng.mti;
-    b.envi[sidx(EI_NI, EI_MTB, e)] = rng.mtb;
   }
+  MHPPO_HD void commit() {  // after rewards (P_WDL) and the observation (P_DELTA, flags)
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      b.ped[sidx(P_NF * NP, P_WDL * NP + p, e)] = ped_[P_WDL][p];
+      b.ped[sidx(P_NF * NP, P_DELTA * NP + p, e)] = ped_[P_DELTA][p];
+      b.pfl[sidx(NP, p, e)] = pfl_[p];
+    }
+  }
+  // env_observe builds this env's observation row in obs_stage() (device: the wave's LDS
+  // image) and store_obs_row writes it to obs [N][OBS_DIM]
+#ifdef __HIP_DEVICE_COMPILE__
+  MHPPO_HD float *obs_stage() const { return obs_lds_row<OBS_DIM>(); }
+  MHPPO_HD void store_obs_row(float *obs) const { store_obs_wave<OBS_DIM>(obs, e, c.N); }
+#else
+  mutable float obs_h[OBS_DIM];
+  float *obs_stage() const { return obs_h; }
+  void store_obs_row(float *obs) const {
+    for (int k = 0; k < OBS_DIM; k++) obs[(size_t)e * OBS_DIM + k] = obs_h[k];
+  }
+#endif
   static constexpr int nC() { return NC; }
   static constexpr int nAV() { return NAV; }
   static constexpr int nS() { return V == V_4CARS2 ? 2 * NAV : NAV; }
@@ -556,21 +646,35 @@ MHPPO_HD inline bool choix_pedestrian(EV &E, const Ped &q, int mode) {
       }
     }
   }
-  MHPPO_UNROLL
-  for (int s = 0; s < E.nC(); s++) {
-    if (!in_view(E, s, mode)) continue;
-    double line = E.car(C_LINE, s);
-    if (is_in_front(E, q, line, 1.0)) {
-      double pos = E.car(C_SC, s);
-      if ((pos < car_size + q.Sx) && (pos > q.Sx)) return false;
-      if (pos < q.Sx) {
-        double car_time = fabs((pos - q.Sx) / (E.car(C_VC, s) + 10e-3));
-        double CG = CG_score(E, q, fabs(q.lpos - line) * E.cross);
-        if (car_time + E.car(C_LIGHT, s) < CG) return false;
+  // Gap acceptance (:162-172): over the in-view cars in slot order, a car in front within
+  // car_size ahead refuses; a car behind the pedestrian draws a CG_score and refuses if its
+  // time gap is shorter; otherwise the next car.  Restated as a loop over the CG draws with a
+  // single CG_score site: each round selects the first slot >= from that blocks or draws.
+  // (Unrolled over slots, a wave would run one inlined CG_score per slot any lane reaches.)
+  int from = 0;
+  for (;;) {
+    int hit = -1;
+    double pos = 0, spd = 0, line = 0, light = 0;
+    MHPPO_UNROLL
+    for (int s = E.nC() - 1; s >= 0; s--) {  // descending: the lowest qualifying slot wins
+      if (s < from || !in_view(E, s, mode)) continue;
+      const double ln = E.car(C_LINE, s), ps = E.car(C_SC, s);
+      if (!is_in_front(E, q, ln, 1.0)) continue;
+      if (((ps < car_size + q.Sx) && (ps > q.Sx)) || (ps < q.Sx)) {
+        hit = s;
+        pos = ps;
+        spd = E.car(C_VC, s);
+        line = ln;
+        light = E.car(C_LIGHT, s);
       }
     }
+    if (hit < 0) return true;
+    if (pos > q.Sx) return false;  // blocking car (pos < car_size + Sx held)
+    double car_time = fabs((pos - q.Sx) / (spd + 10e-3));
+    double CG = CG_score(E, q, fabs(q.lpos - line) * E.cross);
+    if (car_time + light < CG) return false;
+    from = hit + 1;
   }
-  return true;
 }
 
 template <class EV>
@@ -813,12 +917,13 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
     }
     E.car(C_TS, i) = Ts;
     double light = E.car(C_LIGHT, i);
-    if (light < 0.0) {
-      double ne = (Ts < 0) ? -1. * exp(4. * (Ts)) : -1. * (1 + Ts);
-      E.car(C_ES, i) = pymin(ne, E.car(C_ES, i));
-    }
-    if (light > 0.0) {
-      double ne = (q.Sx - Sc > 0) ? -1. * exp(-4. * (q.Sx - Sc)) : -1. * (1 + Sc - q.Sx);
+    // red (:250-253) and green (:254-257) light are exclusive: one exp site serves both
+    if (light < 0.0 || light > 0.0) {
+      const bool red = light < 0.0;
+      const bool ex = red ? (Ts < 0) : (q.Sx - Sc > 0);
+      double ne;
+      if (ex) ne = -1. * exp(red ? 4. * (Ts) : -4. * (q.Sx - Sc));
+      else ne = red ? -1. * (1 + Ts) : -1. * (1 + Sc - q.Sx);
       E.car(C_ES, i) = pymin(ne, E.car(C_ES, i));
     }
   }
@@ -846,7 +951,7 @@ MHPPO_HD inline double car_follow_action(const EV &E, int s, double lead_V, doub
   double diff_dist = lead_S - E.car(C_SC, s);
   double delta_v = speed_car - lead_V;
   double sm = 2. + (speed_car * 2.0) + (speed_car * delta_v) / E.c.idm_den;
-  return E.c.b10 * (1 - pow(speed_car / 10., 4.0) - pow(sm / diff_dist, 2.0));
+  return E.c.b10 * (1 - pow_4(speed_car / 10.) - pow_2(sm / diff_dist));
 }
 
 template <class EV>
@@ -878,7 +983,7 @@ MHPPO_HD inline void car_step(const EV &E, int s, double action, double light) {
   E.car(C_LIGHT, s) = light;
 }
 
-MHPPO_HD inline double car_reward(double Vc) { return -10. * pow(Vc - 10.0, 2.0) / 100.0; }
+MHPPO_HD inline double car_reward(double Vc) { return -10. * pow_2(Vc - 10.0) / 100.0; }
 
 
 #ifdef __HIP__  // HIP translation units (host and device passes), not the host-only simulator

@@ -1,5 +1,5 @@
 """Mean per-dispatch SQ counter values per kernel from rocprofv3 --pmc directories.
-usage: python tools/pmc_sq.py <dir> [<dir> ...]"""
+usage: python tools/pmc_sq.py [--kernel SUBSTR] <dir> [<dir> ...]   (default SUBSTR: mlp_train)"""
 import csv
 import glob
 import os
@@ -7,15 +7,18 @@ import sys
 from collections import defaultdict
 
 
-def main(dirs):
+def main(argv):
+    sub = "mlp_train"
+    if argv[:1] == ["--kernel"]:
+        sub, argv = argv[1], argv[2:]
     per = defaultdict(lambda: defaultdict(list))
-    for d in dirs:
+    for d in argv:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 name = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
                 per[name][(row["Counter_Name"], row.get("Dispatch_Id", ""))].append(float(row["Counter_Value"]))
     for name, cs in sorted(per.items()):
-        if "mlp_train" not in name:
+        if sub not in name:
             continue
         tot = defaultdict(list)
         for (c, _), v in cs.items():
