@@ -287,9 +287,27 @@ MHPPO_HD inline void rng_seed(uint32_t *mt, uint64_t seed) {
   mt[0] = 0x80000000u;
 }
 
+// fmod is exact (the remainder is always representable).  The device's ocml fmod reduces
+// the exponent difference in a loop; with a small quotient (|x/y| < 2^52, the env's lane
+// index) the remainder is one fma away: q = trunc(|x|/|y|) is the true quotient or one too
+// large (the division rounds up onto an integer), and |x| - q|y| is then the exact
+// remainder, which fma returns unrounded.  Same bits as fmod, NaN/inf/zero cases included.
+MHPPO_HD __forceinline__ double fmod_exact(double x, double y) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const double ax = fabs(x), ay = fabs(y);
+  const double q = trunc(ax / ay);
+  if (!(q < 0x1p52) || !(ay > 0.0) || !isfinite(ax) || !isfinite(ay)) return fmod(x, y);
+  double r = fma(-q, ay, ax);
+  if (r < 0.0) r = fma(-(q - 1.0), ay, ax);
+  return copysign(r, x);
+#else
+  return fmod(x, y);
+#endif
+}
+
 // CPython float floor division (Objects/floatobject.c _float_div_mod)
 MHPPO_HD inline double py_floordiv(double vx, double wx) {
-  double mod = fmod(vx, wx);
+  double mod = fmod_exact(vx, wx);
   double div = (vx - mod) / wx;
   if (mod) {
     if ((wx < 0) != (mod < 0)) { mod += wx; div -= 1.0; }
@@ -744,8 +762,17 @@ MHPPO_HD inline void function_step(const EV &E, const Ped &q, double time, doubl
   constexpr int V = EV::VAR;
   if (q.has(F_SIN)) {
     double t = time + E.c.dt;
-    double speed_p = (q.A * sin(q.W * (t - q.t0)) + q.B);
-    double pos_p = ((-E.cl / 2.) + (q.A * (-cos(q.W * (t - q.t0)) + cos(q.W * 0.0)) / q.W));
+    double sn, cs;
+#ifdef __HIP_DEVICE_COMPILE__
+    sincos(q.W * (t - q.t0), &sn, &cs);  // one range reduction: ocml sin/cos/sincos share it (same bits)
+#else
+    sn = sin(q.W * (t - q.t0));
+    cs = cos(q.W * (t - q.t0));
+#endif
+    const double z = q.W * 0.0;
+    const double c0 = z == 0.0 ? 1.0 : cos(z);  // cos(+-0) == 1 exactly; NaN/inf W still go through cos
+    double speed_p = (q.A * sn + q.B);
+    double pos_p = ((-E.cl / 2.) + (q.A * (-cs + c0) / q.W));
     if (!(pos_p >= 0.0 && speed_p < fabs(q.ivy))) {
       pos = (double)q.dir * pos_p;
       spd = (double)q.dir * speed_p;
@@ -798,8 +825,10 @@ MHPPO_HD inline void ped_step(EV &E, Ped &q, double time) {
       double new_spy, new_vpy;
       function_step(E, q, time, new_spy, new_vpy);
       bool change_line = false;
-      if (fabs(new_spy) < cl / 2) {  // will_change_line (:276-281)
-        double new_line = py_floordiv(new_spy + cl / 2, E.cross);
+      // new_spy's lane (:278, and apply_change_line :287 on the same value): one floordiv
+      const bool spy_in = fabs(new_spy) < cl / 2;
+      const double new_line = spy_in ? py_floordiv(new_spy + cl / 2, E.cross) : 0.0;
+      if (spy_in) {  // will_change_line (:276-281)
         if (new_line != q.lpos && fabs(q.Sy) < cl / 2) change_line = true;
       }
       double dtc = ((double)E.c.nb_lines - q.lpos - 1) * E.cross * (double)(q.dir > 0);
@@ -836,10 +865,9 @@ MHPPO_HD inline void ped_step(EV &E, Ped &q, double time) {
         q.Vx = nvx;
         q.ct = q.ct + dt;
         if (change_line && new_choice) {  // apply_change_line (:283-289)
-          if (fabs(new_spy) >= cl / 2) {
+          if (!spy_in) {
             q.lpos = (double)(E.c.nb_lines * (q.dir < 0) - 1 * (q.dir > 0));
           } else {
-            double new_line = py_floordiv(new_spy + cl / 2, E.cross);
             if (new_line != q.lpos) q.lpos = new_line;
           }
         }

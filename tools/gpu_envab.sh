@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest $ARGS -m gpu -x -v --timeout 300 --timeout
 tail -2 $OUT/pytest_gpu.log
 MHPPO_LIB=build_ab/timing/libmhppo.so timeout -k 10 120 python tools/env_phases.py 4cars 4 1 2 65536 > $OUT/env_phases.txt 2>&1 || { tail -20 $OUT/env_phases.txt; exit 1; }
 cat $OUT/env_phases.txt
-bash tools/ab_env.sh base new > $OUT/ab.txt 2>&1 || { tail -20 $OUT/ab.txt; exit 1; }
+bash tools/ab_env.sh ${ABV:-base new} > $OUT/ab.txt 2>&1 || { tail -20 $OUT/ab.txt; exit 1; }
 cat $OUT/ab.txt
