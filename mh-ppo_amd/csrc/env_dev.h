@@ -409,11 +409,19 @@ __device__ __forceinline__ void store_obs_wave(float *obs, int e, int N) {
     for (int k = 0; k < OD; k++) obs[(size_t)e * OD + k] = s[lane * OD + k];
     return;
   }
-  constexpr int NCH = 16 * OD;  // 16-B chunks of the wave's block
-  const float4 *src = reinterpret_cast<const float4 *>(s);
-  float4 *dst = reinterpret_cast<float4 *>(wbase);
+  constexpr int NCH = 16 * OD;  // 16-B chunks of the wave's block: OD/4 per lane (+ a tail)
+  const float4 *src = reinterpret_cast<const float4 *>(s) + lane;
+  float4 *dst = reinterpret_cast<float4 *>(wbase) + lane;
+  // all reads first, into distinct registers, then the stores (no store waits on the
+  // previous one's data registers)
+  float4 v[NCH / 64];
 #pragma unroll
-  for (int q = lane; q < NCH; q += 64) dst[q] = src[q];
+  for (int j = 0; j < NCH / 64; j++) v[j] = src[64 * j];
+#pragma unroll
+  for (int j = 0; j < NCH / 64; j++) dst[64 * j] = v[j];
+  if constexpr (NCH % 64 != 0) {
+    if (lane < NCH % 64) dst[64 * (NCH / 64)] = src[64 * (NCH / 64)];
+  }
 }
 #endif
 
