@@ -28,12 +28,17 @@ Extra JSON fields:
                  work; the fraction of the f32-MFMA peak (157.3) is reported beside it.
                  With MHPPO_TRAIN_EXACT_F32 (ppo.EXACT_F32) the peak is the f32 one.
   roofline_env — the fused sample+env-step kernel: SURVEY §8(d)'s algorithmic bytes per
-                 env-step (cfg3 1515 B, cfg4 1615 B) x N / its mean duration; 8 TB/s.
+                 env-step (cfg3 1515 B, cfg4 1615 B) x N / its mean duration over the timed
+                 region's launches, from HIP events attached to each launch's dispatch
+                 packet (mhppo_kernel_timing_begin/_end: hipExtLaunchKernelGGL start/stop
+                 events, i.e. the kernel's execution as rocprofv3 times it, without the
+                 event packets' queue gaps); 8 TB/s.
   cpu_baseline — the C oracle (same env + rollout, glibc, OpenMP over envs on the box's
                  cores) + the PyTorch-CPU update (same thread count) on a bounded sample
                  of the same workload, rank 0, N=1 only; legs timed separately.
 """
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -170,12 +175,12 @@ def main():
     algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
     ro = algo.rollout
 
-    def iteration(events=None):
-        """Algo_PPO.train's loop body (mhppo/algo.py), with the env-step kernel bracketed."""
+    def iteration():
+        """Algo_PPO.train's loop body (mhppo/algo.py)."""
         ro.reset()
         with torch.no_grad():
             ro.batch = ro.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
-                                      iteration=ro.iteration, step_events=events)
+                                      iteration=ro.iteration)
         ro.iteration += 1
         from mhppo.rollout import bucket_segments
         ro.cross, ro.wait, ro.choice = bucket_segments(ro.batch)
@@ -185,15 +190,18 @@ def main():
 
     for _ in range(a.warmup):
         iteration()
-    events = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(T)]
-              for _ in range(a.steps)]
+    from mhppo import _lib
+    L = _lib.lib()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ppo.TRAIN_EVENTS = []
+    # the env-step launches carry HIP events attached to their dispatch packets
+    # (hipExtLaunchKernelGGL): the kernel's own execution time, as rocprofv3 reports it
+    _lib.check(L.mhppo_kernel_timing_begin(a.steps * T))
     t0 = time.perf_counter()
     for k in range(a.steps):
-        iteration(events[k])
+        iteration()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -204,7 +212,11 @@ def main():
     dt = float(t.item())
     ms = dt / a.steps * 1e3
     value = world * N * T / (dt / a.steps)
-    kern_ms = sum(ev[0].elapsed_time(ev[1]) for evs in events for ev in evs) / (a.steps * T)
+    env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
+    _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(env_ms), ctypes.byref(env_n)))
+    if env_n.value != a.steps * T:
+        raise RuntimeError(f"timed {env_n.value} env-step launches, expected {a.steps * T}")
+    kern_ms = env_ms.value / env_n.value
     S = venv.n_slots
     S_all = 2 * S if variant == "4cars" else S  # car slots incl. the 4cars IDM followers
     per_env = env_step_bytes(S_all, npd, S, venv.obs_dim)

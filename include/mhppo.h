@@ -192,6 +192,14 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
                          mhppo_rollout_bufs *bufs, void *stream);
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
 
+/* Measurement (bench.py): the next `n` env-step launches (mhppo_rollout_sample_env) of the
+ * calling thread carry HIP events attached to their dispatch packets (hipExtLaunchKernelGGL
+ * start/stop events: the kernel's execution, not the queue's event-packet gaps);
+ * mhppo_kernel_timing_end synchronises them and returns the summed milliseconds and the
+ * number of timed launches.  No reference counterpart. */
+int mhppo_kernel_timing_begin(int n);
+int mhppo_kernel_timing_end(double *ms_total, int *launches);
+
 /* Status of the rollout launches queued on `stream` so far: synchronises the stream, reads
  * and clears bufs->status, and returns MHPPO_ENAN when a NaN policy output was drawn from
  * (Categorical(probs) at the episode start, :409; MultivariateNormal(loc) per step, :451:

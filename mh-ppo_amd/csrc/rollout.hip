@@ -12,6 +12,9 @@
 // Update-time kernels (advantage stats/normalise, PPO surrogates, MSE) are
 // elementwise + deterministic two-pass reductions (fixed summation order).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <vector>
 
 #include <algorithm>
 #include <math.h>
@@ -867,6 +870,23 @@ double *scratch(size_t n) {
 
 inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + TPB - 1) / TPB)); }
 
+// Dispatch-attached timing of the env-step launches (mhppo_kernel_timing_begin/_end): the
+// next n launches of the calling thread record a start/stop pair with their dispatch.
+struct KernelTiming {
+  std::vector<hipEvent_t> ev;  // [2 * cap]
+  int cap = 0, used = 0;
+  bool on = false;
+};
+thread_local KernelTiming g_ktime;
+inline bool ktime_next(hipEvent_t &a, hipEvent_t &b) {
+  KernelTiming &k = g_ktime;
+  if (!k.on || k.used >= k.cap) return false;
+  a = k.ev[2 * k.used];
+  b = k.ev[2 * k.used + 1];
+  k.used++;
+  return true;
+}
+
 // register-view rollout step for a compiled shape (4cars2 has no rollout driver)
 template <int V, int NC, int NAV, int NP>
 bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, const mhppo_rollout_bufs &B,
@@ -876,10 +896,19 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
   } else {
     if (!use_reg_view(c, V, NC, NAV, NP)) return false;
     const dim3 g = grid_for(c.N);
-    if (B.rows)
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ktime_next(e0, e1)) {  // same launch, with the timing events attached to its dispatch
+      if (B.rows)
+        hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps,
+                              t, B);
+      else
+        hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps, t,
+                              B);
+    } else if (B.rows) {
       hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
-    else
+    } else {
       hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
+    }
     return true;
   }
 }
@@ -968,6 +997,36 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
   size_t shm = 2 * sizeof(float) * mlp_size(NF_C, 1);
   VLAUNCH(k_policy, c.variant, grid_for(R), shm, (hipStream_t)stream, c, *actor_cross, *actor_wait, *bufs);
   CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_kernel_timing_begin(int n) {
+  if (n < 0) return set_error(MHPPO_EINVAL, "kernel timing: n < 0");
+  KernelTiming &k = g_ktime;
+  for (int i = 2 * k.cap; i < 2 * n; i++) {
+    hipEvent_t e;
+    CHECK_HIP(hipEventCreate(&e));
+    k.ev.push_back(e);
+  }
+  if (n > k.cap) k.cap = n;
+  k.used = 0;
+  k.on = n > 0;
+  return MHPPO_OK;
+}
+
+int mhppo_kernel_timing_end(double *ms_total, int *launches) {
+  KernelTiming &k = g_ktime;
+  double tot = 0.0;
+  for (int i = 0; i < k.used; i++) {
+    CHECK_HIP(hipEventSynchronize(k.ev[2 * i + 1]));
+    float ms = 0.f;
+    CHECK_HIP(hipEventElapsedTime(&ms, k.ev[2 * i], k.ev[2 * i + 1]));
+    tot += ms;
+  }
+  if (ms_total) *ms_total = tot;
+  if (launches) *launches = k.used;
+  k.on = false;
+  k.used = 0;
   return MHPPO_OK;
 }
 
