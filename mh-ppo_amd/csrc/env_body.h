@@ -154,6 +154,7 @@ MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
     if (V == V_SCALABLE) o[k++] = (float)E.car_traffic();
     o[k++] = (float)c.nb_lines;
   }
+  MHPPO_MARK(11);
   MHPPO_UNROLL
   for (int p = 0; p < E.nP(); p++) {
     Ped q = load_ped(E, p);
@@ -166,10 +167,9 @@ MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
       k += 9;
     }
   }
+  MHPPO_MARK(12);
   if constexpr (OD > 0) {
-#ifndef MHPPO_EXP_NO_OBS
     if (obs) E.store_obs_row(obs);
-#endif
   }
 }
 
@@ -336,9 +336,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
       car_step(E, nS + i, a, light);
     }
   }
-#ifndef MHPPO_EXP_NO_COMMIT
   E.commit_cars();
-#endif
   MHPPO_MARK(4);
   MHPPO_UNROLL
   for (int p = 0; p < E.nP(); p++) {
@@ -346,10 +344,16 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     ped_step(E, q, time);
     store_ped(E, p, q, true);
   }
-#ifndef MHPPO_EXP_NO_COMMIT
   E.commit_peds();
-#endif
   MHPPO_MARK(5);
+  // The observation (:825-832, get_state after detection and rewards) reads only fields that
+  // detection and the rewards never write (cars' kinematics/light/line/existence, the
+  // pedestrians' kinematics/flags other than accident/worst-scenario, and the running-min
+  // delta that only get_data itself updates), so it is taken here, right after the
+  // pedestrian step: its wave-coalesced block store then drains while detection and the
+  // rewards compute instead of at the very end of the step.
+  env_observe(E, 1, obs);
+  MHPPO_MARK(8);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) acc[i] = 0.;
   MHPPO_UNROLL
@@ -359,9 +363,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     ped_detection(E, q, prev, acc, add);
     E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
   }
-#ifndef MHPPO_EXP_NO_COMMIT
   E.commit_det();
-#endif
   MHPPO_MARK(6);
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
@@ -386,8 +388,6 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     E.rw[i] = r;
   }
   MHPPO_MARK(7);
-  env_observe(E, 1, obs);
-  MHPPO_MARK(8);
   int d = (time >= c.ep_len) || (E.ped_traffic() <= 0);
   if (done) done[e] = (uint8_t)d;
   b.envd[sidx(E_ND, E_TIME, e)] = time + c.dt;

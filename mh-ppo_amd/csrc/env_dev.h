@@ -42,8 +42,8 @@ namespace mhppo {
 static __device__ unsigned long long g_timing[16];
 // per-wave accumulators in LDS (one global atomic per phase and wave, at MHPPO_MARK_FLUSH)
 __device__ __forceinline__ unsigned long long *timing_slots() {
-  // [wave][phase 1..10 at 1..10, last stamp at 11]: 1.5 KB, within the train kernel's LDS slack
-  __shared__ unsigned long long t_acc[16][12];
+  // [wave][phase 1..14 at 1..14, last stamp at 15]: 2 KB, within the train kernel's LDS slack
+  __shared__ unsigned long long t_acc[16][16];
   return &t_acc[threadIdx.x >> 6][0];
 }
 __device__ __forceinline__ void timing_mark(int k) {
@@ -53,17 +53,17 @@ __device__ __forceinline__ void timing_mark(int k) {
   __builtin_amdgcn_sched_barrier(0);
   if ((threadIdx.x & 63) == 0) {
     if (k > 0) {
-      a[k] += now - a[11];
+      a[k] += now - a[15];
     } else {
-      for (int q = 0; q < 11; q++) a[q] = 0;
+      for (int q = 0; q < 15; q++) a[q] = 0;
     }
-    a[11] = now;
+    a[15] = now;
   }
 }
 __device__ __forceinline__ void timing_flush() {
   unsigned long long *a = timing_slots();
   if ((threadIdx.x & 63) == 0) {
-    for (int q = 1; q < 11; q++)
+    for (int q = 1; q < 15; q++)
       if (a[q]) atomicAdd(&g_timing[q], a[q]);
     atomicAdd(&g_timing[15], 1ull);
   }

@@ -16,8 +16,8 @@ from mhppo.env import VecCrosswalk  # noqa: E402
 from mhppo.models import Model_PPO  # noqa: E402
 
 PHASES = {1: "MT refill (wave)", 2: "env state load (EnvR)", 3: "select + MVN action", 4: "car steps (+IDM)",
-          5: "pedestrian step", 6: "detection", 7: "rewards", 8: "observe", 9: "commit",
-          10: "rollout buffer writes"}
+          5: "pedestrian step", 6: "detection", 7: "rewards", 11: "observe: car rows",
+          12: "observe: ped get_data", 8: "observe: obs block store", 9: "commit", 10: "rollout buffer writes"}
 
 
 def main():
