@@ -1274,6 +1274,8 @@ __global__ void __launch_bounds__(256)
   const int i0 = (int)((int64_t)g * nw / RG), i1 = (int)((int64_t)(g + 1) * nw / RG);
   double s = 0.0;
   if (k < np) {
+    // unrolled: the group's loads issue together (the sum order, and so the bits, unchanged)
+#pragma unroll 16
     for (int i = i0; i < i1; i++) s += (double)gpart[(size_t)i * np + k];
   } else if (k < nd) {
     for (int i = i0; i < i1; i++) s += dpart[(size_t)i * 3 + (k - np)];

@@ -203,29 +203,72 @@ __device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
     v[4 * q + 3] = relu(v[4 * q + 3] + c.w);
   }
 }
-// one 13 -> 32 -> 64 -> 32 -> 1 actor (torch-packed W) into LDS, rows permuted as above
-__device__ void stage(float *L, const float *__restrict__ W, int tid, int nt) {
-  const float *w1 = W, *b1 = w1 + 32 * NF_C, *w2 = b1 + 32, *b2 = w2 + 2048, *w3 = b2 + 64, *b3 = w3 + 2048,
-              *w4 = b3 + 32, *b4 = w4 + 32;
-  for (int x = tid; x < 32 * S1; x += nt) {
-    const int i = x / S1, k = x % S1;
-    L[O_W1 + x] = k < NF_C ? w1[neuron_of_row(i) * NF_C + k] : 0.0f;
+// LDS row holding neuron n (0..31) in the permuted staging above: the inverse of neuron_of_row
+__device__ __forceinline__ int row_of_neuron(int n) {
+  const int m = n >> 1;
+  return (m & 3) + 8 * (m >> 2) + 4 * (n & 1);
+}
+// Both 13 -> 32 -> 64 -> 32 -> 1 actors (torch-packed W) into LDS, [2][HEAD], the weight rows
+// of layers 1-3 permuted as above (LDS row i of a layer holds neuron neuron_of_row(i)), W1 rows
+// zero-padded to S1.  Every global load of both nets is issued first (coalesced, in source
+// order, none waiting on another), then the permuted LDS stores: one memory round trip per
+// block (a strided load -> store loop per array costs ~20 dependent trips per net at the start
+// of every policy launch).
+template <int NT>
+__device__ __forceinline__ void stage_both(float *L, const float *__restrict__ Wa, const float *__restrict__ Wb,
+                                           int tid) {
+  constexpr int NW1 = 32 * NF_C, N1 = (NW1 + NT - 1) / NT, N2 = 2048 / NT;
+  static_assert(2048 % NT == 0 && NT >= 64, "stage_both: block size");
+  const float *W[2] = {Wa, Wb};
+  float v1[2][N1], v2[2][N2], v3[2][N2], vb1[2], vb2[2], vb3[2], vw4[2], vb4[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const float *w1 = W[h], *b1 = w1 + NW1, *w2 = b1 + 32, *b2 = w2 + 2048, *w3 = b2 + 64, *b3 = w3 + 2048,
+                *w4 = b3 + 32, *b4 = w4 + 32;
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int x = tid + q * NT;
+      v1[h][q] = x < NW1 ? w1[x] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      v2[h][q] = w2[tid + q * NT];
+      v3[h][q] = w3[tid + q * NT];
+    }
+    vb1[h] = tid < 32 ? b1[tid] : 0.0f;
+    vb3[h] = tid < 32 ? b3[tid] : 0.0f;
+    vw4[h] = tid < 32 ? w4[tid] : 0.0f;
+    vb2[h] = tid < 64 ? b2[tid] : 0.0f;
+    vb4[h] = tid == 0 ? b4[0] : 0.0f;
   }
-  for (int x = tid; x < 32; x += nt) {
-    L[O_B1 + x] = b1[neuron_of_row(x)];
-    L[O_B3 + x] = b3[neuron_of_row(x)];
-    L[O_W4 + x] = w4[x];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    float *Lh = L + h * HEAD;
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int x = tid + q * NT;
+      if (x < NW1) {
+        const int n = x / NF_C, k = x - n * NF_C;
+        Lh[O_W1 + row_of_neuron(n) * S1 + k] = v1[h][q];
+      }
+    }
+    if (tid < 64) Lh[O_W1 + (tid >> 1) * S1 + NF_C + (tid & 1)] = 0.0f;  // padding columns 13, 14
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      const int x = tid + q * NT;
+      const int n2 = x >> 5, k2 = x & 31;  // W2 [64][32]
+      Lh[O_W2 + ((n2 & 32) + row_of_neuron(n2 & 31)) * S2 + k2] = v2[h][q];
+      const int n3 = x >> 6, k3 = x & 63;  // W3 [32][64]
+      Lh[O_W3 + row_of_neuron(n3) * S3 + k3] = v3[h][q];
+    }
+    if (tid < 32) {
+      Lh[O_B1 + row_of_neuron(tid)] = vb1[h];
+      Lh[O_B3 + row_of_neuron(tid)] = vb3[h];
+      Lh[O_W4 + tid] = vw4[h];
+    }
+    if (tid < 64) Lh[O_B2 + (tid & 32) + row_of_neuron(tid & 31)] = vb2[h];
+    if (tid == 0) Lh[O_B4] = vb4[h];
   }
-  for (int x = tid; x < 64 * 32; x += nt) {
-    const int i = x >> 5, k = x & 31;
-    L[O_W2 + i * S2 + k] = w2[((i & 32) + neuron_of_row(i & 31)) * 32 + k];
-  }
-  for (int x = tid; x < 64; x += nt) L[O_B2 + x] = b2[(x & 32) + neuron_of_row(x & 31)];
-  for (int x = tid; x < 32 * 64; x += nt) {
-    const int i = x >> 6, k = x & 63;
-    L[O_W3 + i * S3 + k] = w3[neuron_of_row(i) * 64 + k];
-  }
-  if (tid == 0) L[O_B4] = b4[0];
 }
 }  // namespace pol
 
@@ -239,8 +282,7 @@ __global__ void __launch_bounds__(TPB) k_policy_mfma(Cfg c, const float *__restr
   const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (tid >> 6)));
   const int nwaves = gridDim.x * (TPB / 64);
   if ((int64_t)gw * 64 < c.N) mt_refill_wave<TPB / 64>(eb, c.N, gw * 64 + l, gw * 64 + l < c.N);
-  stage(lds, Wc, tid, TPB);
-  stage(lds + HEAD, Ww, tid, TPB);
+  stage_both<TPB>(lds, Wc, Ww, tid);
   __syncthreads();
   const int R = c.N * c.nS * c.P;
   const int32_t *__restrict__ rows = B.rows;
