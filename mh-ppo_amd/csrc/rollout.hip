@@ -175,6 +175,13 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
 #ifndef MHPPO_POLICY_BLOCKS_PER_CU
 #define MHPPO_POLICY_BLOCKS_PER_CU 2  // persistent k_policy_mfma blocks per CU (A/B builds override)
 #endif
+#ifndef MHPPO_POLICY_TPB
+// k_policy_mfma block size: 8 waves share one LDS copy of the two actors, so two blocks per CU
+// give four waves per SIMD (<= 128 VGPRs) to hide the MFMA chains' layer-to-layer latency
+// (LDS per block: 38.7 KB of weights + 39.9 KB of MT-refill images)
+#define MHPPO_POLICY_TPB 512
+#endif
+constexpr int PTPB = MHPPO_POLICY_TPB;
 namespace pol {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int S1 = 15, S2 = 33, S3 = 65;  // odd LDS row strides: conflict-free operand reads
@@ -273,16 +280,16 @@ __device__ __forceinline__ void stage_both(float *L, const float *__restrict__ W
 }  // namespace pol
 
 template <int V>
-__global__ void __launch_bounds__(TPB) k_policy_mfma(Cfg c, const float *__restrict__ Wc,
-                                                     const float *__restrict__ Ww, float mean_c, float std_c,
-                                                     float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
+__global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__restrict__ Wc,
+                                                      const float *__restrict__ Ww, float mean_c, float std_c,
+                                                      float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
   using namespace pol;
   extern __shared__ float lds[];  // [2][HEAD]: cross, wait
   const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5;
-  const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (tid >> 6)));
-  const int nwaves = gridDim.x * (TPB / 64);
-  if ((int64_t)gw * 64 < c.N) mt_refill_wave<TPB / 64>(eb, c.N, gw * 64 + l, gw * 64 + l < c.N);
-  stage_both<TPB>(lds, Wc, Ww, tid);
+  const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (PTPB / 64) + (tid >> 6)));
+  const int nwaves = gridDim.x * (PTPB / 64);
+  if ((int64_t)gw * 64 < c.N) mt_refill_wave<PTPB / 64>(eb, c.N, gw * 64 + l, gw * 64 + l < c.N);
+  stage_both<PTPB>(lds, Wc, Ww, tid);
   __syncthreads();
   const int R = c.N * c.nS * c.P;
   const int32_t *__restrict__ rows = B.rows;
@@ -896,14 +903,15 @@ double *scratch(size_t n) {
   return s.p;
 }
 
-#define VLAUNCH(kern, variant, grid, shm, stream, ...)                                                       \
+#define VLAUNCH(kern, variant, grid, shm, stream, ...) VLAUNCHB(kern, variant, grid, dim3(TPB), shm, stream, __VA_ARGS__)
+#define VLAUNCHB(kern, variant, grid, block, shm, stream, ...)                                               \
   do {                                                                                                       \
     switch (variant) {                                                                                       \
-      case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
-      case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;     \
-      case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break; \
-      case V_NAIF: hipLaunchKernelGGL(kern<V_NAIF>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
-      case V_STOP: hipLaunchKernelGGL(kern<V_STOP>, grid, dim3(TPB), shm, stream, __VA_ARGS__); break;       \
+      case V_COOP: hipLaunchKernelGGL(kern<V_COOP>, grid, block, shm, stream, __VA_ARGS__); break;           \
+      case V_4CARS: hipLaunchKernelGGL(kern<V_4CARS>, grid, block, shm, stream, __VA_ARGS__); break;         \
+      case V_SCALABLE: hipLaunchKernelGGL(kern<V_SCALABLE>, grid, block, shm, stream, __VA_ARGS__); break;   \
+      case V_NAIF: hipLaunchKernelGGL(kern<V_NAIF>, grid, block, shm, stream, __VA_ARGS__); break;           \
+      case V_STOP: hipLaunchKernelGGL(kern<V_STOP>, grid, block, shm, stream, __VA_ARGS__); break;           \
       default:                                                                                               \
         return set_error(MHPPO_EINVAL, "the rollout/evaluation drivers do not support variant %d (4cars2: "    \
                          "the reference has no driver and its followers earn no reward)", variant);          \
@@ -1018,12 +1026,13 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
       cus[dev] = n;
     }
+    constexpr size_t WPB = PTPB / 64;  // waves per block
     const size_t tiles = R / 32 + 2, waves_env = ((size_t)c.N + 63) / 64;
-    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + 3) / 4);
-    blocks = std::max<size_t>(blocks, (waves_env + 3) / 4);
-    VLAUNCH(k_policy_mfma, c.variant, dim3((unsigned)blocks), 2 * pol::HEAD * sizeof(float), (hipStream_t)stream, c,
-            actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std, actor_wait->mean,
-            actor_wait->std, *bufs, env_bufs(env));
+    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + WPB - 1) / WPB);
+    blocks = std::max<size_t>(blocks, (waves_env + WPB - 1) / WPB);
+    VLAUNCHB(k_policy_mfma, c.variant, dim3((unsigned)blocks), dim3(PTPB), 2 * pol::HEAD * sizeof(float),
+             (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std,
+             actor_wait->mean, actor_wait->std, *bufs, env_bufs(env));
     CHECK_HIP(hipGetLastError());
     return MHPPO_OK;
   }
