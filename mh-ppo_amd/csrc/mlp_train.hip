@@ -287,19 +287,47 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   // packed torch-layout offsets
   const int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
             G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32 * NOUT, NWP = G_B4 + NOUT;
-  // ---- stage weights (padded strides, zero padding)
-  for (int i = tid; i < 32 * LY::S1; i += 64 * WAVES) {
-    const int r = i / LY::S1, c = i % LY::S1;
-    // FOLD_B1: b1 rides in the padding column nin of W1 against a constant-1 input
-    lds[LY::O_W1 + i] = c < nin ? W[G_W1 + r * nin + c] : ((FOLD_B1 && c == nin) ? W[G_B1 + r] : 0.0f);
+  // ---- stage weights (padded strides, zero padding).  Every global load is issued before
+  // the first LDS store (one memory round trip; a strided load -> store loop per array costs
+  // one dependent trip per iteration, ~24 per launch).
+  {
+    constexpr int NT = 64 * WAVES, N1 = (32 * LY::S1 + NT - 1) / NT, N2 = 2048 / NT;
+    static_assert(2048 % NT == 0 && NT >= 64, "staging: block size");
+    float v1[N1], v2[N2], v3[N2];
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int i = tid + q * NT, r = i / LY::S1, c = i % LY::S1;
+      // FOLD_B1: b1 rides in the padding column nin of W1 against a constant-1 input
+      v1[q] = i >= 32 * LY::S1 ? 0.0f
+                               : (c < nin ? W[G_W1 + r * nin + c] : ((FOLD_B1 && c == nin) ? W[G_B1 + r] : 0.0f));
+    }
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      v2[q] = W[G_W2 + tid + q * NT];
+      v3[q] = W[G_W3 + tid + q * NT];
+    }
+    const float vb1 = tid < 32 ? W[G_B1 + tid] : 0.0f, vb3 = tid < 32 ? W[G_B3 + tid] : 0.0f;
+    const float vb2 = tid < 64 ? W[G_B2 + tid] : 0.0f, vw4 = tid < 32 * NOUT ? W[G_W4 + tid] : 0.0f;
+    const float vb4 = tid < NOUT ? W[G_B4 + tid] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int i = tid + q * NT;
+      if (i < 32 * LY::S1) lds[LY::O_W1 + i] = v1[q];
+    }
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      const int i = tid + q * NT;
+      lds[LY::O_W2 + (i >> 5) * S2 + (i & 31)] = v2[q];
+      lds[LY::O_W3 + (i >> 6) * S3 + (i & 63)] = v3[q];
+    }
+    if (tid < 32) {
+      lds[LY::O_B1 + tid] = vb1;
+      lds[LY::O_B3 + tid] = vb3;
+    }
+    if (tid < 64) lds[LY::O_B2 + tid] = vb2;
+    if (tid < 32 * NOUT) lds[LY::O_W4 + tid] = vw4;
+    if (tid < NOUT) lds[LY::O_B4 + tid] = vb4;
   }
-  for (int i = tid; i < 32; i += 64 * WAVES) lds[LY::O_B1 + i] = W[G_B1 + i];
-  for (int i = tid; i < 64 * 32; i += 64 * WAVES) lds[LY::O_W2 + (i >> 5) * S2 + (i & 31)] = W[G_W2 + i];
-  for (int i = tid; i < 64; i += 64 * WAVES) lds[LY::O_B2 + i] = W[G_B2 + i];
-  for (int i = tid; i < 32 * 64; i += 64 * WAVES) lds[LY::O_W3 + (i >> 6) * S3 + (i & 63)] = W[G_W3 + i];
-  for (int i = tid; i < 32; i += 64 * WAVES) lds[LY::O_B3 + i] = W[G_B3 + i];
-  for (int i = tid; i < 32 * NOUT; i += 64 * WAVES) lds[LY::O_W4 + i] = W[G_W4 + i];
-  if (tid < NOUT) lds[LY::O_B4 + tid] = W[G_B4 + tid];
   __syncthreads();
   float *ws = lds + LY::O_WEND + w * LY::WAVE_LDS;
   float *T0 = ws + LY::O_T, *T1 = T0 + TILE, *T2 = T1 + TILE;
