@@ -950,17 +950,46 @@ __global__ void __launch_bounds__(64 * WAVES)
   constexpr int nin = NIN;
   constexpr int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
                 G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
-  // ---- stage the weights: bf16 images (three parts), b1 as input column 13 of W1
-  for (int i = tid; i < 32 * 16; i += 64 * WAVES) {
-    const int r = i >> 4, c = i & 15;
-    const float v = c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f);
-    stage_w(L8 + O_W1, W1_PART, W1_ROWB, r, c, v);
-  }
-  for (int i = tid; i < 64 * 32; i += 64 * WAVES) stage_w(L8 + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, W[G_W2 + i]);
-  for (int i = tid; i < 32 * 64; i += 64 * WAVES) stage_w(L8 + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, W[G_W3 + i]);
+  // ---- stage the weights: bf16 images (three parts), b1 as input column 13 of W1.  Every
+  // global load is issued before the first LDS store (one memory round trip per launch; a
+  // strided load -> split -> store loop per array costs one dependent trip per iteration).
   float *F = reinterpret_cast<float *>(L8 + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
-  for (int i = tid; i < NF; i += 64 * WAVES)
-    F[i] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
+  {
+    constexpr int NT = 64 * WAVES, N1 = (32 * 16 + NT - 1) / NT, N2 = 2048 / NT, NFQ = (NF + NT - 1) / NT;
+    static_assert(2048 % NT == 0, "staging: block size");
+    float v1[N1], v2[N2], v3[N2], vf[NFQ];
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int i = tid + q * NT, r = i >> 4, c = i & 15;
+      v1[q] = i >= 32 * 16 ? 0.0f : (c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f));
+    }
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      v2[q] = W[G_W2 + tid + q * NT];
+      v3[q] = W[G_W3 + tid + q * NT];
+    }
+#pragma unroll
+    for (int q = 0; q < NFQ; q++) {
+      const int i = tid + q * NT;
+      vf[q] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
+    }
+#pragma unroll
+    for (int q = 0; q < N1; q++) {
+      const int i = tid + q * NT;
+      if (i < 32 * 16) stage_w(L8 + O_W1, W1_PART, W1_ROWB, i >> 4, i & 15, v1[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < N2; q++) {
+      const int i = tid + q * NT;
+      stage_w(L8 + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, v2[q]);
+      stage_w(L8 + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, v3[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NFQ; q++) {
+      const int i = tid + q * NT;
+      if (i < NF) F[i] = vf[q];
+    }
+  }
   __syncthreads();
   char *wb = L8 + O_WAVE + w * WAVE_B;  // this wave's image / f32 transpose slot
   float *T = reinterpret_cast<float *>(wb);
