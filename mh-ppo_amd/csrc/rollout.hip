@@ -690,6 +690,10 @@ __global__ void __launch_bounds__(TPB) k_returns(const double *rew, float *ret, 
 // runs — every record read once and every bucket row written once, in full lines.
 namespace bk {
 constexpr int SEGS = 64, STEPS = 16;
+// LDS strides per segment, padded by one word: phase 1 writes one step of 64 consecutive
+// segments per instruction, and unpadded strides (208 / 16 words) put those 64 lanes on 4
+// banks (16-way conflicts on every record field)
+constexpr int OBS_SEG = STEPS * NF_C + 1, V_SEG = STEPS + 1;
 }
 __global__ void __launch_bounds__(TPB)
     k_bucket_scatter(const int64_t *__restrict__ pos, const int8_t *__restrict__ bucket, int64_t NS, int T,
@@ -697,9 +701,9 @@ __global__ void __launch_bounds__(TPB)
                      const float *__restrict__ ret, const double *__restrict__ rew, mhppo_bucket_dst d0,
                      mhppo_bucket_dst d1) {
   using namespace bk;
-  __shared__ float s_obs[SEGS * STEPS * NF_C];
-  __shared__ float s_v[3][SEGS * STEPS];
-  __shared__ double s_rew[SEGS * STEPS];
+  __shared__ float s_obs[SEGS * OBS_SEG];
+  __shared__ float s_v[3][SEGS * V_SEG];
+  __shared__ double s_rew[SEGS * V_SEG];
   __shared__ int64_t s_pos[SEGS];
   __shared__ int8_t s_b[SEGS];
   const int64_t s0 = (int64_t)blockIdx.x * SEGS;
@@ -715,10 +719,10 @@ __global__ void __launch_bounds__(TPB)
     const int sg = i % SEGS, tl = i / SEGS;
     if (sg >= nseg || tl >= nt || s_pos[sg] < 0) continue;
     const int64_t rec = (int64_t)(t0 + tl) * NS + s0 + sg;
-    const int o = sg * STEPS + tl;  // LDS: segment-major
+    const int o = sg * V_SEG + tl;  // LDS: segment-major
     const float *so = obs + rec * NF_C;
 #pragma unroll
-    for (int j = 0; j < NF_C; j++) s_obs[o * NF_C + j] = so[j];
+    for (int j = 0; j < NF_C; j++) s_obs[sg * OBS_SEG + tl * NF_C + j] = so[j];
     s_v[0][o] = act[rec];
     s_v[1][o] = logp[rec];
     s_v[2][o] = ret[rec];
@@ -733,9 +737,9 @@ __global__ void __launch_bounds__(TPB)
     const mhppo_bucket_dst &D = s_b[sg] ? d1 : d0;
     const int64_t r0 = p * T + t0;
     float *oo = D.obs + r0 * NF_C;
-    for (int j = l; j < nt * NF_C; j += 64) oo[j] = s_obs[sg * STEPS * NF_C + j];
+    for (int j = l; j < nt * NF_C; j += 64) oo[j] = s_obs[sg * OBS_SEG + j];
     if (l < nt) {
-      const int o = sg * STEPS + l;
+      const int o = sg * V_SEG + l;
       D.act[r0 + l] = s_v[0][o];
       D.logp[r0 + l] = s_v[1][o];
       D.ret[r0 + l] = s_v[2][o];
