@@ -453,7 +453,12 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     int sel = 0;
     MHPPO_UNROLL
     for (int p = 0; p < P; p++) {
-      if (V == V_SCALABLE && o[L.ped_off + p * 9 + 7] == 0.0f) continue;
+      // scalable `if exist:` gate (:439) on the observation's exist field; the register view
+      // reads the same flag from its state (pedestrian existence never changes in a step, and
+      // get_data writes exactly that flag there), not a 4-B gather of the obs row
+      if constexpr (V == V_SCALABLE) {
+        if (EV::CNP > 0 ? !(E.pflag(p) & F_EXIST) : o[L.ped_off + p * 9 + 7] == 0.0f) continue;
+      }
       float out = B.out_c[row0 + p];
       loc = t_minimum(loc, out);
       if (out == loc) sel = p;
@@ -476,7 +481,9 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
       for (int k = 0; k < NF_C; k++) fo[k] = fs[k];
     }
     act[i] = (double)a;
-    int cp = B.closest[(size_t)e * S + i];
+    // closest_ped_d starts at pedestrian 0 and only moves to another one: with one (compile-time)
+    // pedestrian it is 0, and the a_d gather below does not wait on the closest[] load
+    const int cp = EV::CNP == 1 ? 0 : B.closest[(size_t)e * S + i];
     act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
   }
   if constexpr (REC_VEC) {  // this env's S records of step t are contiguous and 16-B aligned

@@ -1,4 +1,5 @@
-"""Rollout collect timing (80 steps of policy + env kernels, 65536 4cars envs), HIP events per kernel."""
+"""Rollout collect timing (80 steps of policy + env kernels, 65536 envs; ROLLOUT_CFG selects the
+shape, default 4cars 4/1/2), HIP events per kernel."""
 import os
 import sys
 
@@ -10,7 +11,9 @@ from mhppo.algo import Algo_PPO  # noqa: E402
 from mhppo.env import VecCrosswalk  # noqa: E402
 from mhppo.models import Model_PPO  # noqa: E402
 
-venv = VecCrosswalk("4cars", 65536, 4, 1, 2, seed_base=0)
+# ROLLOUT_CFG="variant nb_car nb_ped nb_lines" (default: the bench's config 3)
+_v, _nc, _np, _nl = (os.environ.get("ROLLOUT_CFG") or "4cars 4 1 2").split()
+venv = VecCrosswalk(_v, 65536, int(_nc), int(_np), int(_nl), seed_base=0)
 torch.manual_seed(0)
 algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
 T = 80
