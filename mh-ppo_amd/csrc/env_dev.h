@@ -914,6 +914,15 @@ template <class EV, class AV>
 MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool add) {
   constexpr int V = EV::VAR;
   const int nS = E.nAV();  // detection runs over the AVs (followers excluded, :845)
+  // green lights of existing AVs behind the pedestrian (:229-233): the loop below never writes
+  // light, position or existence, so the count is the same for every i
+  double clw = 0;
+  if (V != V_NAIF) {
+    MHPPO_UNROLL
+    for (int k = 0; k < nS; k++)
+      if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0))
+        clw += 1.0;
+  }
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
     bool cond = is_in_front(E, q, E.car(C_LINE, i), 0);
@@ -944,11 +953,6 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
     if (V == V_NAIF) {
       if (Sc < q.Sx) Ts = pymax(q.wt + 10. * q.ct - tb + 1., Ts);
     } else {
-      double clw = 0;
-      MHPPO_UNROLL
-      for (int k = 0; k < nS; k++)
-        if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0))
-          clw += 1.0;
       if (Sc < q.Sx) Ts = pymax((1. + clw) * q.wt + 2. * q.ct - tb + 1., Ts);
     }
     E.car(C_TS, i) = Ts;
