@@ -126,3 +126,33 @@ def test_mfma_policy_bit_identical_to_valu(case):
         outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=2, iteration=1)))
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_kernel_timing_events_leave_results_unchanged():
+    """mhppo_kernel_timing_begin/_end (bench.py's env-kernel clock): the timed launches
+    (hipExtLaunchKernelGGL with dispatch-attached events) produce the same episode bit for bit
+    as untimed ones, exactly the requested number of launches is timed, and the time is positive."""
+    import ctypes
+    from mhppo import _lib
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    L = _lib.lib()
+    outs, times = [], []
+    for timed in (False, True):
+        ro = RolloutGPU(VecCrosswalk("4cars", 256, 4, 1, 2, seed_base=11))
+        torch.manual_seed(4)
+        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        ad = Model_PPO(ro.dc, 2, 2).cuda()
+        if timed:
+            _lib.check(L.mhppo_kernel_timing_begin(50))  # fewer than the episode's 80 steps
+        outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=3, iteration=0)))
+        if timed:
+            ms, n = ctypes.c_double(0.0), ctypes.c_int32(0)
+            _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(ms), ctypes.byref(n)))
+            times.append((ms.value, n.value))
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    ms, n = times[0]
+    assert n == 50 and ms > 0.0
