@@ -174,12 +174,14 @@ def n_params(n_in, n_out):
 
 
 def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=None, counts=None, m_global=1.0,
-                exact=None):
+                exact=None, sums=None):
     """Fused forward/loss/backward of one head (mhppo_mlp_train).
     kind 0 (critic): returns (grad, sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
     kind 1 (continuous actor) / 2 (choice actor): returns (grad, sums[3] = (sum surrogate, 0, 0), None).
     grad is the packed torch-layout gradient (W1 b1 .. W4 b4), written into the net's flat
-    .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient."""
+    .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient.
+    `sums`: optional zeroed float64 [3] the kernel accumulates into (train_epoch passes rows of
+    one zeroed tensor: one fill per epoch instead of one per pass)."""
     want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
     if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):
         raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
@@ -197,7 +199,8 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     grad = net.grad_flat()
     if grad.numel() != np_ or grad.device != dev:
         raise ValueError("gradient storage does not match the net / the batch's device")
-    sums = torch.zeros(3, dtype=torch.float64, device=dev)
+    if sums is None:
+        sums = torch.zeros(3, dtype=torch.float64, device=dev)
     w = net.flat()
     p = _lib.ptr
     ev = None
@@ -236,19 +239,22 @@ def train_epoch(heads, bucket=None):
     """One full-batch epoch of every head: critic passes -> ONE all-reduce of all heads'
     advantage sums -> actor passes -> ONE gradient all-reduce -> Adam.  Returns this rank's
     (actor, critic) loss sums per head (float64 [1] tensors)."""
-    crit = [k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m) for h in heads]
-    stats = torch.cat([sc[1:3] for _, sc, _ in crit])
+    H = len(heads)
+    sums = torch.zeros(2 * H, 3, dtype=torch.float64, device=heads[0].obs.device)  # critic rows, actor rows
+    crit = [k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sums[i]) for i, h in enumerate(heads)]
+    stats = sums[:H, 1:3].reshape(-1).contiguous()
     _allreduce_(stats)
     out = []
     for i, (h, (_, sc, V)) in enumerate(zip(heads, crit)):
         st = stats[2 * i:2 * i + 2]
+        sa = sums[H + i]
         if h.kind == "c":
-            _, sa, _ = k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m)
+            k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m, sums=sa)
         elif h.per_row:
-            _, sa, _ = k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, h.act.float(), h.logp, st, None,
-                                   m_global=h.m)
+            k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, h.act.float(), h.logp, st, None, m_global=h.m,
+                        sums=sa)
         else:
-            _, sa, _ = k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, None, h.logp, st, h.counts, m_global=h.m)
+            k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, None, h.logp, st, h.counts, m_global=h.m, sums=sa)
         out.append((sa[0:1], sc[0:1]))
     nets = [n for h in heads for n in (h.actor, h.critic)]
     if bucket is not None:

@@ -60,7 +60,15 @@ def _install_cpu_doubles(ppo):
         f = -torch.minimum(r * A, r.clamp(0.8, 1.2) * A)
         return (f * counts.reshape(1, 2)).sum()
 
-    def mlp_train(kind, net, obs, ret, value=None, act=None, lp_old=None, stats=None, counts=None, m_global=1.0):
+    def mlp_train(kind, net, obs, ret, value=None, act=None, lp_old=None, stats=None, counts=None, m_global=1.0,
+                  sums=None):
+        g, s, v = _mlp_train(kind, net, obs, ret, value, act, lp_old, stats, counts, m_global)
+        if sums is None:
+            return g, s, v
+        sums += s  # the kernel accumulates into the caller's zeroed sums (include/mhppo.h)
+        return g, sums, v
+
+    def _mlp_train(kind, net, obs, ret, value, act, lp_old, stats, counts, m_global):
         m = m_global
         params = list(net.parameters())
         out = torch.squeeze(net(obs), -1)
