@@ -253,19 +253,50 @@ __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const
 template <int KIND>
 constexpr int prefetch_ops() { return KIND == K_CRITIC ? 3 : 6; }  // DMA instructions per prefetch
 
-// Synchronous tile load (ragged last tile of the DMA path; every tile otherwise):
-// ordinary buffer loads, rows past M read as 0.
+// Tile inputs through registers: load_tile_regs issues every load of a 32-row tile (X rows,
+// the s0/s1 targets) with none waiting on another; store_tile_regs writes them to the wave's
+// input slot.  A runtime-trip-count load -> store loop would wait one memory round trip per 64
+// floats (15 per tile at n_in = 30).  Rows past M read as 0 (buffer bounds).
+template <class LY>
+struct TileRegs {
+  float x[(LY::XMAX + 63) / 64];
+  float s0, s1;
+};
+template <int KIND, class LY>
+__device__ __forceinline__ void load_tile_regs(TileRegs<LY> &t, const float *X, int nin, const float *ret,
+                                               const float *V, const float *act, const float *lp, int64_t row0,
+                                               int nrows, int l) {
+  const auto rx = rsrc(X + row0 * nin, (uint32_t)(nrows * nin) * 4);
+#pragma unroll
+  for (int i = 0; i < (LY::XMAX + 63) / 64; i++) {
+    const int q = l + 64 * i;
+    t.x[i] = q < 32 * nin ? bload(rx, 4 * q) : 0.0f;
+  }
+  const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
+  t.s0 = bload(rsrc((l < 32 || KIND == K_CRITIC) ? ret + row0 : V + row0, nb), vo);
+  t.s1 = 0.0f;
+  if (KIND == K_CONT) t.s1 = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
+  if (KIND == K_CHOICE)  // [logp_old 32 | action 32] (the action is read only in per-row mode)
+    t.s1 = bload(rsrc((l < 32 || act == nullptr) ? lp + row0 : act + row0, nb), vo);
+}
+template <int KIND, class LY>
+__device__ __forceinline__ void store_tile_regs(float *slot, const TileRegs<LY> &t, int nin, int l) {
+#pragma unroll
+  for (int i = 0; i < (LY::XMAX + 63) / 64; i++) {
+    const int q = l + 64 * i;
+    if (q < 32 * nin) slot[LY::IN_X + q] = t.x[i];
+  }
+  slot[LY::IN_S0 + l] = t.s0;
+  if (KIND == K_CONT || KIND == K_CHOICE) slot[LY::IN_S1 + l] = t.s1;
+}
+// Synchronous tile load (ragged last tile of the DMA path)
 template <int KIND, class LY>
 __device__ __forceinline__ void load_tile_sync(float *slot, const float *X, int nin, const float *ret,
                                                const float *V, const float *act, const float *lp, int64_t row0,
                                                int nrows, int l) {
-  const auto rx = rsrc(X + row0 * nin, (uint32_t)(nrows * nin) * 4);
-  for (int q = l; q < 32 * nin; q += 64) slot[LY::IN_X + q] = bload(rx, 4 * q);
-  const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
-  slot[LY::IN_S0 + l] = bload(rsrc((l < 32 || KIND == K_CRITIC) ? ret + row0 : V + row0, nb), vo);
-  if (KIND == K_CONT) slot[LY::IN_S1 + l] = bload(rsrc(l < 32 ? act + row0 : lp + row0, nb), vo);
-  if (KIND == K_CHOICE)  // [logp_old 32 | action 32] (the action is read only in per-row mode)
-    slot[LY::IN_S1 + l] = bload(rsrc((l < 32 || act == nullptr) ? lp + row0 : act + row0, nb), vo);
+  TileRegs<LY> t;
+  load_tile_regs<KIND, LY>(t, X, nin, ret, V, act, lp, row0, nrows, l);
+  store_tile_regs<KIND, LY>(slot, t, nin, l);
 }
 
 template <int KIND, int KS, bool PF>
@@ -360,6 +391,9 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
   int cb = 0;
   MHPPO_MARK(0);
   if (PF && gw < nfull) prefetch_tile<KIND, LY>(ws + LY::O_IN, X, ret, V, act, lp_old, gw * 32, l);
+  TileRegs<LY> tnext;  // non-PF: the next tile's inputs in registers
+  if (!PF && gw < ntiles)
+    load_tile_regs<KIND, LY>(tnext, X, nin, ret, V, act, lp_old, gw * 32, (int)min((int64_t)32, M - gw * 32), l);
   for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= (PF ? 1 : 0)) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
@@ -375,7 +409,12 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
         load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
       }
     } else {
-      load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
+      // this tile's inputs were loaded into registers one iteration earlier (the first tile's
+      // before the loop); the next tile's loads are in flight during this tile's compute
+      store_tile_regs<KIND, LY>(slot, tnext, nin, l);
+      const int64_t nt = tile + nw;
+      if (nt < ntiles)
+        load_tile_regs<KIND, LY>(tnext, X, nin, ret, V, act, lp_old, nt * 32, (int)min((int64_t)32, M - nt * 32), l);
     }
     wave_sync();
     MHPPO_MARK(1);  // tile inputs landed
