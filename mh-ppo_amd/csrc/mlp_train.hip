@@ -1361,7 +1361,7 @@ __global__ void __launch_bounds__(64 * WAVES)
 // Deterministic two-stage gradient reduction over the per-wave partials (fixed order,
 // float64): stage 1 sums contiguous groups of waves, stage 2 sums the RG group totals.
 // Slot k < np is gradient k, slots np..np+2 the float64 sums.
-constexpr int RG = 32;
+constexpr int RG = 64;
 
 __global__ void __launch_bounds__(256)
     k_grad_stage1(const float *gpart, const double *dpart, int nw, int np, double *tmp) {
