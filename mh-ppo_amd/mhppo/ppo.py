@@ -261,10 +261,59 @@ def train_epoch(heads, bucket=None):
         bucket.allreduce(nets)
     else:
         _allreduce_net_grads(*nets)
-    for h in heads:
-        h.opt_actor.step()
-        h.opt_critic.step()
+    adam_steps([o for h in heads for o in (h.opt_actor, h.opt_critic)])
     return out
+
+
+def _fused_adam_ok(o):
+    return (isinstance(o, torch.optim.Adam) and getattr(o, "grad_scale", None) is None
+            and getattr(o, "found_inf", None) is None
+            and all(g.get("fused") and not g.get("amsgrad") and not g.get("capturable") and not g.get("differentiable")
+                    and not g.get("decoupled_weight_decay", False) and not isinstance(g["lr"], torch.Tensor)
+                    for g in o.param_groups))
+
+
+def adam_steps(opts):
+    """One step of every optimiser in `opts`, bit-identical to calling o.step() on each.  For
+    fused torch Adams (the GPU path) whose state exists, the steps of all six nets run as ONE
+    step-count increment and one torch._fused_adam_ launch per distinct hyper-parameter set —
+    the same per-tensor kernel arithmetic as each optimiser's own step (torch.optim.adam
+    _fused_adam), in 1 + (distinct lr) launches instead of 2 per optimiser.  Anything else (CPU,
+    the first step, which creates the state, non-default options) takes o.step()."""
+    fast = all(_fused_adam_ok(o) for o in opts)
+    groups, steps = {}, []
+    if fast:
+        for o in opts:
+            for g in o.param_groups:
+                ps = [p for p in g["params"] if p.grad is not None]
+                if any(len(o.state[p]) == 0 for p in ps):
+                    fast = False
+                    break
+                if not ps:
+                    continue
+                key = (ps[0].device, float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]),
+                       float(g["weight_decay"]), float(g["eps"]), bool(g["maximize"]))
+                e = groups.setdefault(key, ([], [], [], [], []))
+                for p in ps:
+                    st = o.state[p]
+                    if p.dtype != torch.float32 or p.device != key[0]:
+                        fast = False
+                    e[0].append(p)
+                    e[1].append(p.grad)
+                    e[2].append(st["exp_avg"])
+                    e[3].append(st["exp_avg_sq"])
+                    e[4].append(st["step"])
+                    steps.append(st["step"])
+            if not fast:
+                break
+    if not fast:
+        for o in opts:
+            o.step()
+        return
+    torch._foreach_add_(steps, 1)
+    for (_, lr, b1, b2, wd, eps, maximize), (ps, gs, ms, vs, sts) in groups.items():
+        torch._fused_adam_(ps, gs, ms, vs, [], sts, amsgrad=False, lr=lr, beta1=b1, beta2=b2, weight_decay=wd,
+                           eps=eps, maximize=maximize, grad_scale=None, found_inf=None)
 
 
 def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):

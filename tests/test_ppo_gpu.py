@@ -172,3 +172,37 @@ def test_philox_normal_2d_equals_rows():
     for r in range(rows):
         _lib.check(L.mhppo_philox_normal(12345, off + r * stride, _lib.ptr(b[r]), cols, _lib.stream_ptr()))
     assert torch.equal(a, b)
+
+
+def test_adam_steps_bit_identical_to_per_optimizer_steps():
+    """ppo.adam_steps (all six nets' fused Adam steps batched by hyper-parameters) gives the same
+    parameters and moments bit for bit as one o.step() per optimiser, over several steps."""
+    from mhppo import ppo
+    from mhppo.models import Model_PPO
+
+    def make():
+        torch.manual_seed(3)
+        nets = [Model_PPO(13, 1, 1, mean=-1.0, std=3.0), Model_PPO(13, 1, 0), Model_PPO(13, 1, 1, mean=-1.0, std=3.0),
+                Model_PPO(13, 1, 0), Model_PPO(30, 2, 2), Model_PPO(30, 1, 0)]
+        nets = [n.cuda() for n in nets]
+        lrs = [3e-4, 1e-3, 3e-4, 1e-3, 1e-4, 2e-3]
+        opts = [torch.optim.Adam(n.parameters(), lr, fused=True) for n, lr in zip(nets, lrs)]
+        return nets, opts
+
+    runs = []
+    for batched in (False, True):
+        nets, opts = make()
+        g = torch.Generator(device="cuda").manual_seed(7)
+        for _ in range(4):
+            for n in nets:
+                for p in n.parameters():
+                    p.grad = torch.randn(p.shape, device="cuda", generator=g)
+            if batched:
+                ppo.adam_steps(opts)
+            else:
+                for o in opts:
+                    o.step()
+        runs.append(([p.detach().cpu() for n in nets for p in n.parameters()],
+                     [o.state[p]["exp_avg_sq"].cpu() for o, n in zip(opts, nets) for p in n.parameters()]))
+    for a, b in zip(runs[0][0] + runs[0][1], runs[1][0] + runs[1][1]):
+        assert torch.equal(a, b)
