@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """MH-PPO hot-path benchmark on MI355X (driver contract: see task README).
 
-One bench "step" = one full PPO iteration on this rank's shard, exactly Algo_PPO.train's
-loop body (Coop-MH-PPO-scalable.py:854-917):
+One bench "step" = one full PPO iteration on this rank's shard: one call of the product's
+Algo_PPO.train(1) (Coop-MH-PPO-scalable.py:854-917), reward-curve file writing off:
     rollout.reset() -> reset N envs + 80 rollout steps (choice head at t=0; per step:
     policy kernel + fused sample/env-step kernel) -> returns scan -> bucketing ->
-    10 joint epochs of the three heads (cross, wait, choice) -> rollout.reset().
+    10 joint epochs of the three heads (cross, wait, choice) -> immediate rewards, the
+    reward-sum all-reduce and its host read (the reward curves) -> rollout.reset().
 Default workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
     Env_hybrid_multi_coop_4cars, 4 AVs (+4 IDM followers), 1 pedestrian, 2 lanes,
     65536 envs per GPU (weak scaling over ranks), T = 80.
@@ -26,7 +27,8 @@ Extra JSON fields:
                  (six bf16 MFMAs per f32 product, f32-level accuracy), so its
                  ceiling is the bf16 dense MFMA peak / 6 = 419.4 TFLOP/s of f32-equivalent
                  work; the fraction of the f32-MFMA peak (157.3) is reported beside it.
-                 With MHPPO_TRAIN_EXACT_F32 (ppo.EXACT_F32) the peak is the f32 one.
+                 With --exact-f32 (Algo_PPO(exact_f32=True): the f32-MFMA kernel) the peak is
+                 the f32 one.
   roofline_env — the fused sample+env-step kernel: SURVEY §8(d)'s algorithmic bytes per
                  env-step (cfg3 1515 B, cfg4 1615 B) x N / its mean duration over the timed
                  region's launches, from HIP events attached to each launch's dispatch
@@ -100,6 +102,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--save-nets", default=None, help="rank 0 saves every net's flat weights here (tests)")
+    ap.add_argument("--exact-f32", action="store_true",
+                    help="continuous heads on the exact f32-MFMA train kernel (Algo_PPO(exact_f32=True))")
     return ap.parse_args()
 
 
@@ -172,21 +176,11 @@ def main():
     N, T = a.envs, 80
     venv = VecCrosswalk(variant, N, nc, npd, nl, seed_base=0, env_id_offset=rank * N, device=f"cuda:{local}")
     torch.manual_seed(0)
-    algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
-    ro = algo.rollout
+    algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0, save_curves=False, exact_f32=a.exact_f32)
 
     def iteration():
-        """Algo_PPO.train's loop body (mhppo/algo.py)."""
-        ro.reset()
-        with torch.no_grad():
-            ro.batch = ro.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
-                                      iteration=ro.iteration)
-        ro.iteration += 1
-        from mhppo.rollout import bucket_segments
-        ro.cross, ro.wait, ro.choice = bucket_segments(ro.batch)
-        ro.gpu.check()
-        algo.update()
-        ro.reset()
+        """One product training iteration (mhppo/algo.py Algo_PPO.train)."""
+        algo.train(1)
 
     for _ in range(a.warmup):
         iteration()
@@ -227,7 +221,7 @@ def main():
     tr_rows = sum(m for _, _, m, _, _ in tr)
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
-    split = not ppo.EXACT_F32
+    split = not algo.exact_f32
     peak = X3_MFMA_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
     traffic = (pmc_traffic("k_mlp_train_x3<0", "k_mlp_train_x3<1") if split else
                pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>"))

@@ -140,8 +140,9 @@ typedef struct mhppo_rollout_bufs {
     uint8_t *exist;
     int32_t *rows;
     int32_t T, flags;   /* flags: MHPPO_ROLLOUT_* */
-    uint32_t *status;   /* optional device word (caller zeroes it): bit 0 = a NaN choice probability,
-                           bit 1 = a NaN continuous action mean was sampled; see mhppo_rollout_check */
+    uint32_t *status;   /* optional device word, zeroed by mhppo_rollout_begin (flags of the current
+                           episode only): bit 0 = a NaN choice probability, bit 1 = a NaN continuous
+                           action mean was sampled; see mhppo_rollout_check */
 } mhppo_rollout_bufs;
 /* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
  * instead of the MFMA kernel; both are bit-identical (A/B and tests) */
@@ -193,8 +194,9 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
 
 /* Measurement (bench.py): the next `n` env-step launches (mhppo_rollout_sample_env) of the
- * calling thread carry HIP events attached to their dispatch packets (hipExtLaunchKernelGGL
- * start/stop events: the kernel's execution, not the queue's event-packet gaps);
+ * calling thread on the device current at this call carry HIP events attached to their dispatch
+ * packets (hipExtLaunchKernelGGL start/stop events: the kernel's execution, not the queue's
+ * event-packet gaps);
  * mhppo_kernel_timing_end synchronises them and returns the summed milliseconds and the
  * number of timed launches.  No reference counterpart. */
 int mhppo_kernel_timing_begin(int n);
@@ -215,6 +217,13 @@ int mhppo_philox_normal_2d(uint64_t seed, uint64_t offset, uint64_t stride, floa
                            int64_t cols, void *stream);
 
 /* ---- returns / advantage / PPO losses (futur_rewards :658-684, train_model_c/_d :778-851) ---- */
+
+/* The rollout policy heads' float transcendentals (csrc/libm_glibc.h: glibc 2.35's tanhf, expm1f,
+ * expf restated so the device returns glibc's bits — the functions the reference's batch-1 CPU
+ * forward calls, Model_PPO :81-89) evaluated on the float bit patterns first .. first + n - 1
+ * (mod 2^32): the device side of their exhaustive pin (tests/test_libm_gpu.py).
+ * fn: 0 tanhf, 1 expm1f, 2 expf.  out float [n]. */
+int mhppo_libm_eval(int fn, uint64_t first, int64_t n, float *out, void *stream);
 
 /* Segmented reverse discounted scan, G_t = r_t + gamma*G_{t+1} in float64, one segment of
  * T per row: rew float64 [B,T] -> ret float32 [B,T]. */

@@ -756,11 +756,11 @@ constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
 constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
 // per-wave slot: the tile image (also the f32 transpose image), two input slots (double
-// buffered), the float64 loss sums, the two-wave kernel's row-sum accumulators
-constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, O_RACC = O_DACC + 96 * 8,
-              WAVE_B = O_RACC + 5 * 64 * 4;
-constexpr int lds_bytes(int waves) { return O_WAVE + waves * WAVE_B; }
-static_assert(lds_bytes(8) <= 160 * 1024, "LDS budget");
+// buffered), the float64 loss sums
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_DACC + 96 * 8;
+constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
+constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
 
 #ifdef MHPPO_X3_PHASE
@@ -842,30 +842,12 @@ __device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
       " %0, %2, %4, %0\n\t" OP " %0, %1, %5, %0\n\t" OP " %0, %1, %4, %0"                              \
       : "+a"(c)                                                                                      \
       : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2]))
-// AG = false (two waves per SIMD, 256 registers for everything): the compiler's MFMAs
-template <bool AG>
-__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) {
-  if constexpr (AG) X3_MACC6("v_mfma_f32_32x32x16_bf16");
-  else c = mfma6(a, b, c);
-}
-template <bool AG>
-__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) {
-  if constexpr (AG) X3_MACC6("v_mfma_f32_16x16x32_bf16");
-  else c = mfma6_16(a, b, c);
-}
+__device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6("v_mfma_f32_32x32x16_bf16"); }
+__device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6("v_mfma_f32_16x16x32_bf16"); }
 #undef X3_MACC6
 // before the accumulators are read: the last MFMA's result latency (>= 18 passes)
-template <bool AG>
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
-  if constexpr (AG)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
-}
-// Hide a tile's values from common-subexpression elimination (two-wave kernel): the compiler
-// would otherwise keep a forward-pass split (1.5x the registers) alive until the identical
-// split for the backward image, instead of the f32 tile it holds anyway for the ReLU masks.
-__device__ __forceinline__ void opaque(f32x16 &v) {
-#pragma unroll
-  for (int r = 0; r < 16; r++) asm volatile("" : "+v"(v[r]));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
 }
 __device__ __forceinline__ uint2 lds_u2(const char *p) { return *reinterpret_cast<const uint2 *>(p); }
 __device__ __forceinline__ uint2 tr16(const char *p) {
@@ -968,20 +950,18 @@ __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 }
 }  // namespace x3
 
-// WAVES = 4: one wave per SIMD (512 registers: the weight-gradient accumulators and the
-// loop-invariant weight fragments sit in AGPRs).  WAVES = 8: two waves per SIMD, 256 registers
-// for everything — no hoisted fragments, h1 recomputed for the backward, the bias-gradient
-// row sums accumulated in LDS.  Measured alternatives: two tiles per wave in lock
+// One wave per SIMD (512 registers: the weight-gradient accumulators and the loop-invariant
+// weight fragments sit in AGPRs).  Measured alternatives: two waves per SIMD at
+// 256 registers (no hoisted fragments, h1 recomputed: 12 % slower), two tiles per wave in lock
 // step (spills), a software-pipelined loop (backward of tile i beside the forward of tile i+1:
 // 10 % slower).
-template <int KIND, int WAVES>
-__global__ void __launch_bounds__(64 * WAVES)
+template <int KIND>
+__global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
                    float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
                    const double *__restrict__ stats, double m_global, float out_mean, float out_std,
                    float *__restrict__ gpart, double *__restrict__ dpart) {
   using namespace x3;
-  constexpr bool W8 = WAVES == 8, AG = !W8;
   extern __shared__ float lds[];
   char *L8 = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, l = tid & 63;
@@ -1046,21 +1026,18 @@ __global__ void __launch_bounds__(64 * WAVES)
   const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
   const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
   const float b40 = uniform_f(F[128]);
-  // Loop-invariant weight fragments read from LDS once (one wave per SIMD): the backward W^T
-  // ones, and for the critic pass the forward ones too (the actor pass's loss needs those
-  // registers)
-  constexpr bool HF = !W8 && KIND == K_CRITIC, HB = !W8;
+  // Loop-invariant weight fragments read from LDS once: the backward W^T ones, and for the
+  // critic pass the forward ones too (the actor pass's loss needs those registers)
+  constexpr bool HF = KIND == K_CRITIC;
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
   if constexpr (HF) {
     for (int t = 0; t < 2; t++)
       for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
     for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   }
-  if constexpr (HB) {
-    for (int t = 0; t < 2; t++)
-      for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
-    for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
-  }
+  for (int t = 0; t < 2; t++)
+    for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
+  for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
   auto fw2 = [&](int t, int s) -> F3 {
     if constexpr (HF) return wf2[t][s];
     else return w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
@@ -1069,28 +1046,13 @@ __global__ void __launch_bounds__(64 * WAVES)
     if constexpr (HF) return wf3[s];
     else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   };
-  auto bw3 = [&](int t, int s) -> F3 {
-    if constexpr (HB) return wb3[t][s];
-    else return w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
-  };
-  auto bw2 = [&](int s) -> F3 {
-    if constexpr (HB) return wb2[s];
-    else return w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
-  };
+  auto bw3 = [&](int t, int s) -> F3 { return wb3[t][s]; };
+  auto bw2 = [&](int s) -> F3 { return wb2[s]; };
   f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
   f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  // bias-gradient row sums (lane j, half kh: the half-tile sums of feature j): registers, or
-  // lane-private LDS cells in the two-wave kernel
+  // bias-gradient row sums (lane j, half kh: the half-tile sums of feature j)
   float gsum[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // gB2a gB2b gB3 gW4 gB4
-  float *racc = reinterpret_cast<float *>(wb + O_RACC) + l;
-  if constexpr (W8) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) racc[64 * k] = 0.0f;
-  }
-  auto radd = [&](int k, float v) {
-    if constexpr (W8) atomicAdd(racc + 64 * k, v);  // lane-private: no contention, no return
-    else gsum[k] += v;
-  };
+  auto radd = [&](int k, float v) { gsum[k] += v; };
   double *dacc = reinterpret_cast<double *>(wb + O_DACC) + j;
   if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
   float meanf = 0.f, stdf = 1.f;
@@ -1213,23 +1175,19 @@ __global__ void __launch_bounds__(64 * WAVES)
     x3_phase();
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
     const F3 d3f0 = split_step(d3, 0), d3f1 = split_step(d3, 1);
-    if constexpr (W8) {
-      opaque(h2a);
-      opaque(h2b);
-    }
     img_write(imw, d3f0, d3f1);
     lds_order();
     const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
     lds_order();
     img_write(imw, split_step(h2a, 0), split_step(h2a, 1));
     lds_order();
-    macc6<AG>(ad0, img_read(imr, 0), gW3a);
-    macc6<AG>(ad1, img_read(imr, 1), gW3a);
+    macc6(ad0, img_read(imr, 0), gW3a);
+    macc6(ad1, img_read(imr, 1), gW3a);
     lds_order();
     img_write(imw, split_step(h2b, 0), split_step(h2b, 1));
     lds_order();
-    macc6<AG>(ad0, img_read(imr, 0), gW3b);
-    macc6<AG>(ad1, img_read(imr, 1), gW3b);
+    macc6(ad0, img_read(imr, 0), gW3b);
+    macc6(ad1, img_read(imr, 1), gW3b);
     lds_order();
     x3_phase();
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
@@ -1249,11 +1207,6 @@ __global__ void __launch_bounds__(64 * WAVES)
     radd(1, half_row_sum(T, l));
     lds_order();
     x3_phase();
-    // two waves per SIMD: h1 is recomputed here rather than held through layers 2-3
-    if constexpr (W8) {
-      lds_order();
-      h1 = layer1();
-    }
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
     f32x16 d1 = zero16();
     {
@@ -1267,16 +1220,16 @@ __global__ void __launch_bounds__(64 * WAVES)
       lds_order();
       img_write(imw, f0, f1);
       lds_order();
-      macc6<AG>(img_read(imr, 0), bh0, gW2a);
-      macc6<AG>(img_read(imr, 1), bh1, gW2a);
+      macc6(img_read(imr, 0), bh0, gW2a);
+      macc6(img_read(imr, 1), bh1, gW2a);
       lds_order();
       const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
       d1 = mfma6(bw2(2), f2, d1);
       d1 = mfma6(bw2(3), f3, d1);
       img_write(imw, f2, f3);
       lds_order();
-      macc6<AG>(img_read(imr, 0), bh0, gW2b);
-      macc6<AG>(img_read(imr, 1), bh1, gW2b);
+      macc6(img_read(imr, 0), bh0, gW2b);
+      macc6(img_read(imr, 1), bh1, gW2b);
       lds_order();
     }
     relu_mask(d1, h1);
@@ -1296,18 +1249,14 @@ __global__ void __launch_bounds__(64 * WAVES)
         xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
       }
       const F3 b = split8(xv);
-      macc6_16<AG>(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
-      macc6_16<AG>(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
+      macc6_16(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
+      macc6_16(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
     }
     lds_order();
     x3_phase();
   }
   // ---- write this wave's partial gradient (packed torch layout)
-  macc_drain<AG>(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
-  if constexpr (W8) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) gsum[k] = racc[64 * k];
-  }
+  macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
   float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
   float *gp = gpart + (size_t)gw * NWP;
 #pragma unroll
@@ -1412,16 +1361,6 @@ void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int n
 }
 }  // namespace
 
-// waves per block of the split-precision kernel: 4 (one per SIMD); MHPPO_X3_WAVES=8 for A/B runs
-int x3_waves() {
-  static int w = 0;
-  if (!w) {
-    const char *e = getenv("MHPPO_X3_WAVES");
-    w = (e && atoi(e) == 8) ? 8 : 4;
-  }
-  return w;
-}
-
 #ifdef MHPPO_TIMING
 // A/B timing builds only (not in include/mhppo.h): copy out and clear this TU's g_timing
 extern "C" int mhppo_debug_timing_train(unsigned long long *out16) {
@@ -1464,7 +1403,7 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     wk.cus = cus;
   }
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
-  const int waves = split ? x3_waves() : (pf ? 8 : 4);
+  const int waves = split ? x3::WAVES : (pf ? 8 : 4);
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
   const int64_t tiles = (M + 31) / 32;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
@@ -1484,16 +1423,11 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   const dim3 grid((unsigned)blocks);
 #define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
   if (split) {
-#define X3_LAUNCH(KIND_, W_)                                                                                \
-  hipLaunchKernelGGL((k_mlp_train_x3<KIND_, W_>), grid, dim3(64 * W_), x3::lds_bytes(W_), s, packed, X, M, ret, value, \
+#define X3_LAUNCH(KIND_)                                                                                    \
+  hipLaunchKernelGGL((k_mlp_train_x3<KIND_>), grid, dim3(64 * x3::WAVES), x3::LDS_BYTES, s, packed, X, M, ret, value, \
                      act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
-    if (waves == 8) {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 8);
-      else X3_LAUNCH(K_CONT, 8);
-    } else {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, 4);
-      else X3_LAUNCH(K_CONT, 4);
-    }
+    if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC);
+    else X3_LAUNCH(K_CONT);
 #undef X3_LAUNCH
   } else if (pf) {
     if (kind == K_CRITIC)

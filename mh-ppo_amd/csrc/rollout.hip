@@ -24,6 +24,7 @@
 #include "common.h"
 #include "env_body.h"
 #include "rollout_dev.h"
+#include "libm_glibc.h"
 
 using namespace mhppo;
 
@@ -66,7 +67,7 @@ __global__ void __launch_bounds__(TPB)
   mlp_forward<0, 2>(lds, dc, f, pr);
   // Softmax over the pair (Model_PPO type 2, :81-85)
   float mx = pr[0] > pr[1] ? pr[0] : pr[1];
-  float e0 = expf(pr[0] - mx), e1 = expf(pr[1] - mx);
+  float e0 = mhppo_expf(pr[0] - mx), e1 = mhppo_expf(pr[1] - mx);
   float s = e0 + e1;
   float p0 = e0 / s, p1 = e1 / s;
   B.probs_d[r * 2] = p0;
@@ -114,7 +115,7 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
   float out;
   mlp_forward<NF_C, 1>(W, NF_C, f, &out);
   // Model_PPO type 1: tanh(x) * std + mean (:87-89), two roundings
-  float t = tanhf(out) * m.std;
+  float t = mhppo_tanhf(out) * m.std;
   B.out_c[r] = t + m.mean;
 }
 
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
   if (L.scalable && ex == 0.0f) return;  // `if exist:` gate of the scalable driver (:439)
   const float out = mlp_forward13_rows(head ? Ww : Wc, f);
   // Model_PPO type 1: tanh(x) * std + mean (:87-89), two roundings
-  const float t = tanhf(out) * (head ? std_w : std_c);
+  const float t = mhppo_tanhf(out) * (head ? std_w : std_c);
   B.out_c[r] = t + (head ? mean_w : mean_c);
 }
 
@@ -360,7 +361,7 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
     }
     const float out = y + Wl[O_B4];
     if (valid && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)
-      const float t = tanhf(out) * (head ? std_w : std_c);  // Model_PPO type 1 (:87-89)
+      const float t = mhppo_tanhf(out) * (head ? std_w : std_c);  // Model_PPO type 1 (:87-89)
       B.out_c[r] = t + (head ? mean_w : mean_c);
     }
   }
@@ -583,7 +584,7 @@ __global__ void __launch_bounds__(TPB) k_eval_step(Cfg c, Bufs eb, mhppo_mlp mc,
         obs_car_ped_d(o, L, i, p, fd);
         mlp_forward<0, 2>(Wd, dc, fd, pr);
         float mx = pr[0] > pr[1] ? pr[0] : pr[1];
-        float e0 = expf(pr[0] - mx), e1 = expf(pr[1] - mx);
+        float e0 = mhppo_expf(pr[0] - mx), e1 = mhppo_expf(pr[1] - mx);
         float sm = e0 + e1;
         ad[i * P + p] = (e1 / sm > e0 / sm) ? 1 : 0;  // torch.argmax: first maximum
       }
@@ -607,7 +608,7 @@ __global__ void __launch_bounds__(TPB) k_eval_step(Cfg c, Bufs eb, mhppo_mlp mc,
         float out;
         mlp_forward<NF_C, 1>(wait ? Ww : Wc, NF_C, f, &out);
         const mhppo_mlp &m = wait ? mw : mc;
-        float tt = tanhf(out) * m.std;
+        float tt = mhppo_tanhf(out) * m.std;
         cand = (double)(tt + m.mean);
       }
       if (cand < a) a = cand;  // Python min keeps the first on ties (:205-206)
@@ -656,6 +657,15 @@ __global__ void __launch_bounds__(TPB) k_philox(uint64_t seed, uint64_t off, flo
   } else {
     out[i] = (float)(c4[0] >> 8) * (1.0f / 16777216.0f);
   }
+}
+
+// The policy heads' glibc-exact transcendentals (libm_glibc.h) over float bit patterns
+// first .. first + n - 1 (mod 2^32): the device side of their exhaustive pin (mhppo_libm_eval)
+__global__ void __launch_bounds__(TPB) k_libm_eval(int fn, uint64_t first, int64_t n, float *out) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const float x = __uint_as_float((uint32_t)(first + (uint64_t)i));
+  out[i] = fn == 0 ? mhppo_tanhf(x) : (fn == 1 ? mhppo_expm1f(x) : mhppo_expf(x));
 }
 
 // rows x cols standard normals, element (r, c) from counter off + r * stride + c (one
@@ -932,16 +942,20 @@ double *scratch(size_t n) {
 inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + TPB - 1) / TPB)); }
 
 // Dispatch-attached timing of the env-step launches (mhppo_kernel_timing_begin/_end): the
-// next n launches of the calling thread record a start/stop pair with their dispatch.
+// next n launches of the calling thread on the device current at _begin record a start/stop
+// pair with their dispatch.  The events belong to that device (recreated when _begin runs on
+// another one) and are reused across begin/end pairs (2 * the largest n, per thread).
 struct KernelTiming {
   std::vector<hipEvent_t> ev;  // [2 * cap]
-  int cap = 0, used = 0;
+  int cap = 0, used = 0, dev = -1;
   bool on = false;
 };
 thread_local KernelTiming g_ktime;
 inline bool ktime_next(hipEvent_t &a, hipEvent_t &b) {
   KernelTiming &k = g_ktime;
   if (!k.on || k.used >= k.cap) return false;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != k.dev) return false;  // a launch on another device: untimed
   a = k.ev[2 * k.used];
   b = k.ev[2 * k.used + 1];
   k.used++;
@@ -1000,6 +1014,9 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
     return set_error(MHPPO_EINVAL, "choice actor must be %d -> 2 (got %d -> %d)", choice_dim(c), actor_choice->n_in,
                      actor_choice->n_out);
   hipStream_t s = (hipStream_t)stream;
+  // the NaN flags cover this episode only (a flag left by an unchecked earlier collect must not
+  // surface at a later, clean iteration's mhppo_rollout_check)
+  if (bufs->status) CHECK_HIP(hipMemsetAsync(bufs->status, 0, sizeof(uint32_t), s));
   int rc = mhppo_env_reset(env, bufs->obs, stream);
   if (rc) return rc;
   size_t R = (size_t)c.N * c.nS * c.P;
@@ -1065,30 +1082,40 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
 int mhppo_kernel_timing_begin(int n) {
   if (n < 0) return set_error(MHPPO_EINVAL, "kernel timing: n < 0");
   KernelTiming &k = g_ktime;
-  for (int i = 2 * k.cap; i < 2 * n; i++) {
+  k.on = false;
+  k.used = 0;
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  if (dev != k.dev) {  // events of another device: replace them
+    for (hipEvent_t e : k.ev) (void)hipEventDestroy(e);
+    k.ev.clear();
+    k.cap = 0;
+    k.dev = dev;
+  }
+  while ((int)k.ev.size() < 2 * n) {
     hipEvent_t e;
     CHECK_HIP(hipEventCreate(&e));
     k.ev.push_back(e);
   }
   if (n > k.cap) k.cap = n;
-  k.used = 0;
   k.on = n > 0;
   return MHPPO_OK;
 }
 
 int mhppo_kernel_timing_end(double *ms_total, int *launches) {
   KernelTiming &k = g_ktime;
+  const int used = k.used;
+  k.on = false;  // off before anything can fail: later launches are untimed either way
+  k.used = 0;
   double tot = 0.0;
-  for (int i = 0; i < k.used; i++) {
+  for (int i = 0; i < used; i++) {
     CHECK_HIP(hipEventSynchronize(k.ev[2 * i + 1]));
     float ms = 0.f;
     CHECK_HIP(hipEventElapsedTime(&ms, k.ev[2 * i], k.ev[2 * i + 1]));
     tot += ms;
   }
   if (ms_total) *ms_total = tot;
-  if (launches) *launches = k.used;
-  k.on = false;
-  k.used = 0;
+  if (launches) *launches = used;
   return MHPPO_OK;
 }
 
@@ -1170,6 +1197,14 @@ int mhppo_philox_uniform(uint64_t seed, uint64_t offset, float *out, int64_t n, 
   if (!out || n < 0) return set_error(MHPPO_EINVAL, "bad argument");
   if (n == 0) return MHPPO_OK;
   hipLaunchKernelGGL(k_philox, grid_for(n), dim3(TPB), 0, (hipStream_t)stream, seed, offset, out, n, 0);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_libm_eval(int fn, uint64_t first, int64_t n, float *out, void *stream) {
+  if (!out || n < 0 || fn < 0 || fn > 2) return set_error(MHPPO_EINVAL, "bad argument (fn 0 tanhf, 1 expm1f, 2 expf)");
+  if (n == 0) return MHPPO_OK;
+  hipLaunchKernelGGL(k_libm_eval, grid_for(n), dim3(TPB), 0, (hipStream_t)stream, fn, first, n, out);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

@@ -78,6 +78,7 @@ _SIGS = {
     "mhppo_philox_normal": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_uniform": (I32, [U64, U64, P, I64, P]),
     "mhppo_philox_normal_2d": (I32, [U64, U64, U64, P, I64, I64, P]),
+    "mhppo_libm_eval": (I32, [I32, U64, I64, P, P]),
     "mhppo_returns_scan": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_returns_scan_tm": (I32, [P, P, I64, I32, F64, P]),
     "mhppo_bucket_scatter": (I32, [P, P, I64, I32] + [P] * 7),

@@ -180,6 +180,11 @@ class Algo_PPO:
         # lane fix is an env option: VecCrosswalk(..., fix_scalable_lanes=True).
         self.fix_bucket = False
         self.fix_choice_loss = False
+        # continuous heads trained on the exact f32-MFMA kernel (k-ordered fmaf sums) instead of the
+        # default bf16x3 split-precision one (f32-level products at 2.67x the f32-MFMA ceiling)
+        self.exact_f32 = False
+        # reward curves written to load_model/parameters at the end of train() (:908-916)
+        self.save_curves = True
         for k, v in hyperparameters.items():
             setattr(self, k, v)
 
@@ -201,11 +206,13 @@ class Algo_PPO:
             heads, names = [], []
             if m_c > 0:  # the reference trains a continuous head only on a non-empty batch (:869, :874)
                 heads.append(ppo.Head("c", self.actor_net_cross, self.critic_net_cross, self.optimizer_actor_cross,
-                                      self.optimizer_critic_cross, c["obs"], c["act"], c["logp"], c["ret"], m_c))
+                                      self.optimizer_critic_cross, c["obs"], c["act"], c["logp"], c["ret"], m_c,
+                                      exact=self.exact_f32))
                 names.append("cross")
             if m_w > 0:
                 heads.append(ppo.Head("c", self.actor_net_wait, self.critic_net_wait, self.optimizer_actor_wait,
-                                      self.optimizer_critic_wait, w["obs"], w["act"], w["logp"], w["ret"], m_w))
+                                      self.optimizer_critic_wait, w["obs"], w["act"], w["logp"], w["ret"], m_w,
+                                      exact=self.exact_f32))
                 names.append("wait")
             if m_d > 0:  # never empty in the reference (>= 1 existing car per episode); it would raise there
                 heads.append(ppo.Head("d", self.actor_net_choice, self.critic_net_choice, self.optimizer_actor_choice,
@@ -271,7 +278,7 @@ class Algo_PPO:
                 print("Number Cross is ==> {} and Number Wait is ==> {} ".format(int(m_c), int(m_w)))
             self.rollout.reset()
             self.total_loop = self.total_loop + 1
-        if _rank() == 0:
+        if _rank() == 0 and self.save_curves:
             self.save_reward_curves()
         if self.verbose and _rank() == 0:
             print("Complete")

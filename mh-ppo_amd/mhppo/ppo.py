@@ -3,8 +3,8 @@ Coop-MH-PPO-scalable.py:778-851), full batch, on the GPU.
 
 Every head's epoch runs on the fused training kernel (mhppo_mlp_train, csrc/mlp_train.hip;
 the 13-input heads on its bf16x3 split-precision MFMA path — six bf16 products per f32
-product, f32-level accuracy — or, with EXACT_F32 / MHPPO_TRAIN_EXACT_F32, on f32 MFMA with
-k-ordered sums; the choice head on f32 MFMA): a critic pass (forward, MSE gradient, advantage sums) and an
+product, f32-level accuracy — or, with Algo_PPO(exact_f32=True) (MHPPO_TRAIN_EXACT_F32), on f32
+MFMA with k-ordered sums; the choice head on f32 MFMA): a critic pass (forward, MSE gradient, advantage sums) and an
 actor pass (forward, clip-surrogate gradient against the advantage normalised with
 the start-of-epoch critic, backward, weight gradients); Adam (fused) steps each net.
 Epoch semantics follow the reference: the advantage uses the critic of the start of
@@ -67,15 +67,28 @@ class GradBucket:
             self.span[id(net)] = (off, off + n)
             off += n
 
+    def runs(self, nets):
+        """The maximal contiguous spans of the bucket covered by `nets`' gradients, in order (a
+        net that is not trained this epoch — an empty head — splits the span: its stale slice is
+        never reduced)."""
+        spans = sorted(self.span[id(n)] for n in nets)
+        out = []
+        for lo, hi in spans:
+            if out and out[-1][1] == lo:
+                out[-1][1] = hi
+            else:
+                out.append([lo, hi])
+        return [tuple(r) for r in out]
+
     def allreduce(self, nets):
-        """In-place SUM over the smallest contiguous span covering `nets`' gradients."""
+        """In-place SUM of `nets`' gradients: one collective per maximal contiguous run (one for
+        the usual all-heads epoch)."""
         if not _dp() or not nets:
             return
         for n in nets:  # re-link any .grad that autograd / zero_grad rebound
             n.grad_flat()
-        lo = min(self.span[id(n)][0] for n in nets)
-        hi = max(self.span[id(n)][1] for n in nets)
-        dist.all_reduce(self.buf[lo:hi], op=dist.ReduceOp.SUM)
+        for lo, hi in self.runs(nets):
+            dist.all_reduce(self.buf[lo:hi], op=dist.ReduceOp.SUM)
 
 
 def _allreduce_net_grads(*nets):
@@ -163,10 +176,10 @@ FLOPS_PER_ROW_CONT = flops_per_row(13, 1)
 N_IN_MAX = 64  # the fused kernel's widest input (scalable 8-slot choice head: dc = 54)
 
 KIND_CRITIC, KIND_CONT, KIND_CHOICE = 0, 1, 2
-TRAIN_EXACT_F32 = 0x100  # MHPPO_TRAIN_EXACT_F32: the f32-MFMA kernel (k-ordered fmaf sums) for the 13-input heads
-# When True, every fused pass uses the exact f32-MFMA kernel instead of the split-precision
-# bf16 one (include/mhppo.h mhppo_mlp_train); Algo_PPO(exact_f32=True) sets it.
-EXACT_F32 = False
+# MHPPO_TRAIN_EXACT_F32 (include/mhppo.h mhppo_mlp_train): the 13-input heads' passes on the f32-MFMA
+# kernel (k-ordered fmaf sums, the exact f32 arithmetic of an fmaf chain) instead of the default
+# bf16x3 split-precision one; per head: Head(exact=True), set by Algo_PPO(exact_f32=True)
+TRAIN_EXACT_F32 = 0x100
 
 
 def n_params(n_in, n_out):
@@ -174,14 +187,16 @@ def n_params(n_in, n_out):
 
 
 def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=None, counts=None, m_global=1.0,
-                exact=None, sums=None):
+                exact=False, sums=None):
     """Fused forward/loss/backward of one head (mhppo_mlp_train).
     kind 0 (critic): returns (grad, sums[3] = (sum (V-G)^2, sum A, sum A^2), V).
     kind 1 (continuous actor) / 2 (choice actor): returns (grad, sums[3] = (sum surrogate, 0, 0), None).
     grad is the packed torch-layout gradient (W1 b1 .. W4 b4), written into the net's flat
     .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient.
     `sums`: optional zeroed float64 [3] the kernel accumulates into (train_epoch passes rows of
-    one zeroed tensor: one fill per epoch instead of one per pass)."""
+    one zeroed tensor: one fill per epoch instead of one per pass).
+    exact: the f32-MFMA kernel instead of the split-precision one (13-input heads; the choice
+    heads always run on f32 MFMA)."""
     want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
     if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):
         raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
@@ -207,7 +222,7 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     if TRAIN_EVENTS is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    flags = TRAIN_EXACT_F32 if (EXACT_F32 if exact is None else exact) else 0
+    flags = TRAIN_EXACT_F32 if exact else 0
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().mhppo_mlp_train(
             kind | flags, net.n_in, p(w), p(obs), M, p(ret), p(V), p(act), p(logp_old), p(stats), p(counts),
@@ -224,15 +239,17 @@ class Head:
     """One actor/critic pair, its Adam optimisers and this rank's shard of its batch.
     kind "c": continuous head (train_model_c, :778-815); "d": choice head (train_model_d,
     :818-851) with the GLOBAL action counts (n0, n1) of the M x M broadcast, or the
-    opt-in per-row loss.  m = the global row count."""
+    opt-in per-row loss.  m = the global row count.  exact: the continuous head's
+    passes on the exact f32-MFMA kernel (Algo_PPO(exact_f32=True))."""
 
     def __init__(self, kind, actor, critic, opt_actor, opt_critic, obs, act, logp, ret, m, counts=None,
-                 per_row=False):
+                 per_row=False, exact=False):
         self.kind, self.actor, self.critic = kind, actor, critic
         self.opt_actor, self.opt_critic = opt_actor, opt_critic
         self.obs, self.act, self.logp, self.ret, self.m = obs, act, logp, ret, float(m)
         self.counts = None if counts is None else counts.double().contiguous()
         self.per_row = per_row
+        self.exact = bool(exact)
 
 
 def train_epoch(heads, bucket=None):
@@ -241,7 +258,8 @@ def train_epoch(heads, bucket=None):
     (actor, critic) loss sums per head (float64 [1] tensors)."""
     H = len(heads)
     sums = torch.zeros(2 * H, 3, dtype=torch.float64, device=heads[0].obs.device)  # critic rows, actor rows
-    crit = [k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sums[i]) for i, h in enumerate(heads)]
+    crit = [k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sums[i], exact=h.exact)
+            for i, h in enumerate(heads)]
     stats = sums[:H, 1:3].reshape(-1).contiguous()
     _allreduce_(stats)
     out = []
@@ -249,7 +267,7 @@ def train_epoch(heads, bucket=None):
         st = stats[2 * i:2 * i + 2]
         sa = sums[H + i]
         if h.kind == "c":
-            k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m, sums=sa)
+            k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m, sums=sa, exact=h.exact)
         elif h.per_row:
             k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, h.act.float(), h.logp, st, None, m_global=h.m,
                         sums=sa)
@@ -265,8 +283,17 @@ def train_epoch(heads, bucket=None):
     return out
 
 
+def _no_step_hooks(o):
+    """No optimizer step hooks (per instance or global): the fast path bypasses Optimizer.step."""
+    from torch.optim import optimizer as _opt
+    return not (getattr(o, "_optimizer_step_pre_hooks", None) or getattr(o, "_optimizer_step_post_hooks", None)
+                or getattr(_opt, "_global_optimizer_pre_hooks", None)
+                or getattr(_opt, "_global_optimizer_post_hooks", None))
+
+
 def _fused_adam_ok(o):
-    return (isinstance(o, torch.optim.Adam) and getattr(o, "grad_scale", None) is None
+    return (hasattr(torch, "_fused_adam_") and hasattr(torch, "_foreach_add_") and _no_step_hooks(o)
+            and isinstance(o, torch.optim.Adam) and getattr(o, "grad_scale", None) is None
             and getattr(o, "found_inf", None) is None
             and all(g.get("fused") and not g.get("amsgrad") and not g.get("capturable") and not g.get("differentiable")
                     and not g.get("decoupled_weight_decay", False) and not isinstance(g["lr"], torch.Tensor)
@@ -279,7 +306,11 @@ def adam_steps(opts):
     step-count increment and one torch._fused_adam_ launch per distinct hyper-parameter set —
     the same per-tensor kernel arithmetic as each optimiser's own step (torch.optim.adam
     _fused_adam), in 1 + (distinct lr) launches instead of 2 per optimiser.  Anything else (CPU,
-    the first step, which creates the state, non-default options) takes o.step()."""
+    the first step, which creates the state, non-default options, registered optimizer step
+    hooks, a torch without the private torch._fused_adam_ op) takes o.step().  The fast path
+    reads each group's lr at every call, so an LR scheduler's changes apply; it does not run
+    Optimizer.step itself (no step hooks — hence the fallback above — and no scheduler
+    step-order bookkeeping).  Pinned by test_adam_steps_bit_identical_to_per_optimizer_steps."""
     fast = all(_fused_adam_ok(o) for o in opts)
     groups, steps = {}, []
     if fast:
@@ -316,10 +347,11 @@ def adam_steps(opts):
                            eps=eps, maximize=maximize, grad_scale=None, found_inf=None)
 
 
-def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global):
+def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, exact=False):
     """One full-batch epoch of Algo_PPO.train_model_c (:778-815) for one head.
     Returns this rank's (actor, critic) loss sums (float64 tensors)."""
-    return train_epoch([Head("c", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global)])[0]
+    return train_epoch([Head("c", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global,
+                             exact=exact)])[0]
 
 
 def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row=False):

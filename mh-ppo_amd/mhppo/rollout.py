@@ -173,8 +173,9 @@ def returns_scan_tm(rew_tm, gamma=0.99):
     T = rew_tm.shape[0]
     r = rew_tm.reshape(T, -1).contiguous()
     out = torch.empty(r.shape, dtype=torch.float32, device=rew_tm.device)
-    _lib.check(_lib.lib().mhppo_returns_scan_tm(_lib.ptr(r), _lib.ptr(out), r.shape[1], T, gamma,
-                                                _lib.stream_ptr()))
+    with torch.cuda.device(rew_tm.device):  # the records' device and its current stream
+        _lib.check(_lib.lib().mhppo_returns_scan_tm(_lib.ptr(r), _lib.ptr(out), r.shape[1], T, gamma,
+                                                    _lib.stream_ptr(device=rew_tm.device)))
     return out.reshape(rew_tm.shape)
 
 
@@ -183,7 +184,9 @@ def returns_scan(rew, gamma=0.99):
     T = rew.shape[-1]
     r = rew.reshape(-1, T).contiguous()
     out = torch.empty(r.shape, dtype=torch.float32, device=rew.device)
-    _lib.check(_lib.lib().mhppo_returns_scan(_lib.ptr(r), _lib.ptr(out), r.shape[0], T, gamma, _lib.stream_ptr()))
+    with torch.cuda.device(rew.device):
+        _lib.check(_lib.lib().mhppo_returns_scan(_lib.ptr(r), _lib.ptr(out), r.shape[0], T, gamma,
+                                                 _lib.stream_ptr(device=rew.device)))
     return out.reshape(rew.shape)
 
 

@@ -181,6 +181,14 @@ class OracleBatch:
         lib().oracle_batch_step(self.h, _p(a), _p(o), _p(r), _p(rl), _p(d), None if dm is None else _p(dm), _p(mti))
         return o, r, rl, d.astype(bool), dm, mti
 
+    def dump(self):
+        """f64 [n, dump_dim]: every env's internal state as it stands (oracle_env_dump)."""
+        L = lib()
+        L.oracle_batch_dump.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        dm = np.zeros((self.n, self.dump_dim), np.float64)
+        L.oracle_batch_dump(self.h, _p(dm))
+        return dm
+
     def rng_state(self):
         mt = np.zeros((self.n, 624), np.uint32)
         mti = np.zeros(self.n, np.int32)

@@ -9,6 +9,7 @@
  * Used for the full-scale GPU-vs-oracle parity test and the all-core CPU
  * baseline ("the C restatement with OpenMP over envs").
  */
+#include <math.h>
 #include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -109,6 +110,12 @@ void oracle_batch_step(OBatch *b, const double *actions, float *obs, double *rew
     }
 }
 
+/* dump f64 [n, dk]: every env's oracle_env_dump (state as it stands, e.g. after a rollout) */
+void oracle_batch_dump(const OBatch *b, double *dump) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < b->n; i++) oracle_env_dump(b->e[i], dump + (size_t)i * b->dk);
+}
+
 /* mt u32 [n, 624], mti i32 [n] */
 void oracle_batch_get_rng(const OBatch *b, uint32_t *mt, int32_t *mti) {
 #pragma omp parallel for schedule(static)
@@ -133,5 +140,18 @@ void oracle_batch_rollout(OBatch *b, int T, const float *w_cross, const float *w
                                probs + 2 * sp, a_d + sp, logp_d + sp, closest + (size_t)i * S,
                                exist + (size_t)i * S, obs_c + st * 13, act + st, logp + st, rew + st,
                                ep_min + (size_t)i * S);
+    }
+}
+
+/* glibc's own tanhf / expm1f / expf (fn 0 / 1 / 2) on the float bit patterns first .. first + n - 1
+ * (mod 2^32): the reference values the device restatements (mh-ppo_amd/csrc/libm_glibc.h) are
+ * compared with bit for bit (tests/test_libm_gpu.py). */
+void oracle_libm_eval(int fn, uint64_t first, int64_t n, float *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        const uint32_t u = (uint32_t)(first + (uint64_t)i);
+        float x;
+        memcpy(&x, &u, 4);
+        out[i] = fn == 0 ? tanhf(x) : (fn == 1 ? expm1f(x) : expf(x));
     }
 }

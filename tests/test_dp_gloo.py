@@ -61,7 +61,7 @@ def _install_cpu_doubles(ppo):
         return (f * counts.reshape(1, 2)).sum()
 
     def mlp_train(kind, net, obs, ret, value=None, act=None, lp_old=None, stats=None, counts=None, m_global=1.0,
-                  sums=None):
+                  sums=None, exact=False):
         g, s, v = _mlp_train(kind, net, obs, ret, value, act, lp_old, stats, counts, m_global)
         if sums is None:
             return g, s, v
@@ -143,10 +143,12 @@ def test_dp2_equals_single_process():
         np.testing.assert_allclose(a, b, rtol=0, atol=2e-6)
 
 
-def _run_joint(rank, world, port, data, shards, out_q):
+def _run_joint(rank, world, port, data, shards, out_q, skip=()):
     """Three heads (cross, wait, choice) trained by ppo.train_epoch with a GradBucket: two
     collectives per joint epoch.  `shards[rank]` gives this rank's [lo, hi) rows per head
-    (an empty range = an empty shard that must still join every collective)."""
+    (an empty range = an empty shard that must still join every collective).  Heads in `skip`
+    are not trained at all (Algo_PPO.update drops a head whose GLOBAL batch is empty): their
+    gradient slices hold a sentinel that no collective may touch."""
     sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
     from mhppo import ppo
     from mhppo.models import Model_PPO
@@ -161,6 +163,10 @@ def _run_joint(rank, world, port, data, shards, out_q):
     opts = [torch.optim.Adam(n.parameters(), 3e-4 if i % 2 == 0 else 1e-3) for i, n in enumerate(nets)]
     heads = []
     for h, kind in enumerate(("c", "c", "d")):
+        if h in skip:
+            for n in nets[2 * h:2 * h + 2]:
+                n.grad_flat().fill_(1.0)
+            continue
         obs, act, lp, ret = (torch.tensor(x) for x in data[h])
         lo, hi = shards[rank][h]
         m = ppo.global_count(hi - lo, "cpu")
@@ -172,16 +178,17 @@ def _run_joint(rank, world, port, data, shards, out_q):
     for _ in range(3):
         ppo.train_epoch(heads, bucket)
     if rank == 0:
-        out_q.put([p.detach().numpy().copy() for n in nets for p in n.parameters()])
+        out_q.put([p.detach().numpy().copy() for n in nets for p in n.parameters()] +
+                  [nets[2 * h + k].grad_flat().numpy().copy() for h in skip for k in (0, 1)])
     if world > 1:
         dist.destroy_process_group()
 
 
-def _spawn_joint(world, data, shards):
+def _spawn_joint(world, data, shards, skip=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 30600 + os.getpid() % 1000 + world
-    procs = [ctx.Process(target=_run_joint, args=(r, world, port, data, shards, q)) for r in range(world)]
+    port = 30600 + os.getpid() % 1000 + world + 7 * len(skip)
+    procs = [ctx.Process(target=_run_joint, args=(r, world, port, data, shards, q, skip)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
@@ -204,3 +211,30 @@ def test_dp2_joint_epoch_with_empty_shard():
     dp2 = _spawn_joint(2, data, [[(0, 230), (0, 120), (0, 40)], [(230, 500), (120, 120), (40, 90)]])
     for a, b in zip(single, dp2):
         np.testing.assert_allclose(a, b, rtol=0, atol=2e-6)
+
+
+def test_dp2_joint_epoch_skipped_middle_head():
+    """The wait head (the middle nets of the gradient bucket) is empty on every rank, so
+    Algo_PPO.update does not train it: the bucket all-reduce covers the cross and the choice
+    gradients in two runs and never sums the wait head's stale slice (it keeps its sentinel,
+    not world_size x it); the trained nets equal one process."""
+    from mhppo.ppo import GradBucket
+    from mhppo.models import Model_PPO
+    nets = [Model_PPO(13, 1, 1), Model_PPO(13, 1, 0), Model_PPO(13, 1, 1), Model_PPO(13, 1, 0), Model_PPO(20, 2, 2),
+            Model_PPO(20, 1, 0)]
+    b = GradBucket(nets, "cpu")
+    r = b.runs([nets[0], nets[1], nets[4], nets[5]])
+    assert len(r) == 2 and r[0][0] == 0 and r[1][1] == b.buf.numel() and r[0][1] < r[1][0]
+    assert b.runs(nets) == [(0, b.buf.numel())]
+    rng = np.random.default_rng(4)
+    data = []
+    for M, nin, choice in ((300, 13, False), (1, 13, False), (80, 20, True)):
+        act = ((rng.uniform(size=M) < 0.4).astype(np.float32) if choice else rng.normal(-1, 1, M).astype(np.float32))
+        data.append((rng.normal(0, 3, (M, nin)).astype(np.float32), act, rng.normal(-0.6, 0.3, M).astype(np.float32),
+                     rng.normal(-20, 8, M).astype(np.float32)))
+    single = _spawn_joint(1, data, [[(0, 300), (0, 0), (0, 80)]], skip=(1,))
+    dp2 = _spawn_joint(2, data, [[(0, 140), (0, 0), (0, 30)], [(140, 300), (0, 0), (30, 80)]], skip=(1,))
+    for a, b_ in zip(single, dp2):
+        np.testing.assert_allclose(a, b_, rtol=0, atol=2e-6)
+    for g in dp2[-2:]:  # the skipped head's gradient slices: untouched by any collective
+        assert np.all(g == 1.0)

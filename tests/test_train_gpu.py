@@ -31,13 +31,13 @@ NETS = ("actor_net_cross", "actor_net_wait", "actor_net_choice", "critic_net_cro
         "critic_net_choice")
 
 
-def _algo(g):
+def _algo(g, exact_f32=False):
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
     venv = VecCrosswalk(str(g["variant"]), int(g["E"]), int(g["nb_car"]), int(g["nb_ped"]), int(g["nb_lines"]),
                         seed_base=int(g["seed_base"]))
-    algo = Algo_PPO(Model_PPO, venv, verbose=True)
+    algo = Algo_PPO(Model_PPO, venv, verbose=True, exact_f32=exact_f32)
     for n in NETS:
         pre = f"{n}_init_"
         getattr(algo, n).load_state_dict({k[len(pre):]: torch.tensor(g[k]) for k in g.files if k.startswith(pre)})
@@ -79,12 +79,14 @@ def test_bucketed_batch_matches_reference(path):
     np.testing.assert_allclose(d["ret"].cpu().numpy(), g["rtgs_choice"], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("exact", [False, True], ids=["bf16x3", "exact_f32"])
 @pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f)[6:-4] for f in FILES])
-def test_update_on_reference_batch_matches_reference(path):
+def test_update_on_reference_batch_matches_reference(path, exact):
     """Algo_PPO.update (10 joint epochs, fused kernels, bucketed collectives) on the
-    reference's own batch -> the reference's final weights of all six nets."""
+    reference's own batch -> the reference's final weights of all six nets; on the default
+    split-precision train kernel and on the exact f32-MFMA one (Algo_PPO(exact_f32=True))."""
     g = np.load(path)
-    algo = _algo(g)
+    algo = _algo(g, exact)
     dev = algo.venv.device
     t = lambda k, dt=torch.float32: torch.tensor(g[k], dtype=dt, device=dev)  # noqa: E731
     r = algo.rollout

@@ -1,7 +1,8 @@
 """The fused training kernel at the bench's scale: one epoch of the critic and of the
 continuous actor (mhppo_mlp_train kinds 0 and 1) on the bench workload's real bucketed
 batch (4cars 4/1/2, 65 536 envs x 80 steps -> the cross head's ~10.5 M rows, 2 048
-per-wave partial gradients folded by k_grad_stage1/2) against a float64 torch autograd of
+per-wave partial gradients folded by k_grad_stage1/2) — on the default split-precision kernel and on
+the exact f32-MFMA one (exact_f32) — against a float64 torch autograd of
 the same losses (train_model_c, Coop-MH-PPO-scalable.py:778-815) on the same weights.
 Bar: max|dg| <= 1e-4 max|g| for every gradient; the loss sums within 1e-6 relative (the
 advantage sum, which cancels, within 1e-6 of sum|A|)."""
@@ -41,7 +42,8 @@ def _flat_grad(net, loss):
     return torch.cat([g.reshape(-1) for g in gs])
 
 
-def test_fused_epoch_at_bench_scale_vs_float64_autograd():
+@pytest.mark.parametrize("exact", [False, True], ids=["bf16x3", "exact_f32"])
+def test_fused_epoch_at_bench_scale_vs_float64_autograd(exact):
     from mhppo import ppo
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
@@ -59,7 +61,7 @@ def test_fused_epoch_at_bench_scale_vs_float64_autograd():
     m = float(M)
     # ---- critic pass (kind 0): MSE gradient, (sum (V-G)^2, sum A, sum A^2), V
     critic, actor = algo.critic_net_cross, algo.actor_net_cross
-    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m, exact=exact)
     gc, sc = gc.clone(), sc.clone()
     c64 = _f64(critic)
     V64 = torch.squeeze(c64(obs.double()), -1)
@@ -73,7 +75,7 @@ def test_fused_epoch_at_bench_scale_vs_float64_autograd():
     assert abs(float(sc[2]) - float((A64 * A64).sum())) <= 1e-6 * float((A64 * A64).sum())
     # ---- actor pass (kind 1): clip surrogate against A normalised with the epoch's critic
     stats = sc[1:3].clone()
-    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, V, act, lp, stats, m_global=m)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, V, act, lp, stats, m_global=m, exact=exact)
     ga = ga.clone()
     a64 = _f64(actor)
     mean = float(stats[0]) / m

@@ -16,7 +16,6 @@ ap.add_argument("--rows", type=int, default=10485760)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--exact", action="store_true", help="the exact f32-MFMA kernel (MHPPO_TRAIN_EXACT_F32)")
 a = ap.parse_args()
-ppo.EXACT_F32 = a.exact
 M = a.rows
 torch.manual_seed(0)
 actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
@@ -26,16 +25,16 @@ ret = torch.randn(M, device="cuda") * 8 - 20
 act = torch.randn(M, device="cuda") - 1
 lp = torch.randn(M, device="cuda") * 0.3 - 0.9
 for kind in (0, 1, 0, 1):
-    gc, sc, V = ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M))
-    ga, sa, _ = ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M))
+    gc, sc, V = ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M), exact=a.exact)
+    ga, sa, _ = ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M), exact=a.exact)
 torch.cuda.synchronize()
 for kind in (0, 1):
     ppo.TRAIN_EVENTS = []
     for _ in range(a.reps):
         if kind == 0:
-            ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M))
+            ppo.k_mlp_train(0, critic, obs, ret, m_global=float(M), exact=a.exact)
         else:
-            ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M))
+            ppo.k_mlp_train(1, actor, obs, ret, V, act, lp, sc[1:3].clone(), m_global=float(M), exact=a.exact)
     torch.cuda.synchronize()
     ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
     tf = ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12

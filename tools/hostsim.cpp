@@ -30,6 +30,16 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
   return h;
 }
+void hs_destroy(HostEnv *h) {
+  if (!h) return;
+  free(h->b.car);
+  free(h->b.ped);
+  free(h->b.pfl);
+  free(h->b.envd);
+  free(h->b.envi);
+  free(h->b.mt);
+  delete h;
+}
 int hs_obs_dim(HostEnv *h) { return h->c.obs_dim; }
 int hs_state_dim(HostEnv *h) { return 21 * h->c.P + 8 * h->c.nC + 4; }
 #define HS_DISPATCH(call)                                     \
