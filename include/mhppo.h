@@ -104,6 +104,17 @@ int mhppo_env_step(mhppo_env *env, const double *actions, float *obs, double *re
  * [per ped 20][per car slot 8][cross, time, ped_traffic, car_traffic][per ped exist]. */
 int mhppo_env_state_dim(const mhppo_env *env);
 int mhppo_env_get_state(mhppo_env *env, double *out, void *stream);
+/* Per-env event counters since the env's last reset (SURVEY §5 Metrics): the reference's only
+ * run-time diagnostics are five prints inside pedestrian.detection; each one the reference would
+ * print increments the env's counter instead (no device printf).  out uint32 [N, MHPPO_EV_N]. */
+#define MHPPO_EV_ACCIDENT 0  /* "Accident! : "                scalable :186, 4cars :293, coop :185 */
+#define MHPPO_EV_POSSIBLE 1  /* "Possible accident! "         scalable :200, 4cars :307, coop :199 */
+#define MHPPO_EV_SMALL 2     /* "Small mistake - priority ? " scalable :222, 4cars :320, coop :221 */
+#define MHPPO_EV_NOTWAIT 3   /* "Pedestrian is not waiting "  scalable :227, 4cars :325, coop :226
+                                (once per pedestrian; naif :224 every time) */
+#define MHPPO_EV_GREEN 4     /* "Mauvais signal vert "        scalable :236, 4cars :334, coop :235 */
+#define MHPPO_EV_N 5
+int mhppo_env_events(mhppo_env *env, uint32_t *out, void *stream);
 /* RNG cursor: mt uint32 [N, 624], mti int32 [N] (device). */
 int mhppo_env_get_rng(mhppo_env *env, uint32_t *mt, int32_t *mti, void *stream);
 

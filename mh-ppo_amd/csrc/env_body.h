@@ -182,6 +182,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   E.cross = E.rng.uniform(c.xb0, c.xb1);
   E.cl = (double)c.nb_lines * E.cross;
   b.envd[sidx(E_ND, E_CROSS, e)] = E.cross;
+  for (int k = 0; k < EV_N; k++) b.ev[sidx(EV_N, k, e)] = 0u;  // counters are per episode
   for (int p = 0; p < c.P; p++) {
     Ped q;
     ped_init(E, q, 0, 0);
@@ -361,7 +362,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     Ped q = load_ped(E, p);
     bool add = q.has(F_ISCROSS) && (V != V_SCALABLE || q.has(F_EXIST));
     ped_detection(E, q, prev, acc, add);
-    E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA)) | (q.fl & (F_ACCIDENT | F_WSA));
+    E.pflag(p) = (E.pflag(p) & ~(F_ACCIDENT | F_WSA | F_PNW)) | (q.fl & (F_ACCIDENT | F_WSA | F_PNW));
   }
   E.commit_det();
   MHPPO_MARK(6);

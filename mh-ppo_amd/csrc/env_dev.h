@@ -97,12 +97,17 @@ enum : uint32_t {
   F_ACCIDENT = 1u << 4, F_STOP = 1u << 5, F_WSA = 1u << 6, F_NEEDSTOP = 1u << 7,
   F_EXIST = 1u << 8, F_ISCROSS = 1u << 9, F_FOLLOW = 1u << 10, F_DIRNEG = 1u << 11,
   F_DIRPOS = 1u << 12, F_GENDER = 1u << 13, F_SIN = 1u << 14,
+  F_PNW = 1u << 15,  // ped_not_waiting (:35, :224-226): only gates the "Pedestrian is not waiting" print
   F_AGE_SHIFT = 16, F_AGE_MASK = 3u << 16,
   F_TSTOP_SHIFT = 20, F_TSTOP_MASK = 0xFFu << 20,
 };
 // env scalars
 enum { E_CROSS, E_TIME, E_ND };
 enum { EI_PEDTRAF, EI_CARTRAF, EI_MTI, EI_MTB, EI_H0NF, EI_H1NF, EI_NI };
+// Per-env event counters: the reference's only run-time diagnostics are prints inside
+// pedestrian.detection (scalable :186, :200, :222, :227, :236; 4cars :293-334); each print
+// here increments this env's counter, cleared by reset.  Order = include/mhppo.h MHPPO_EV_*.
+enum { EV_ACCIDENT, EV_POSSIBLE, EV_SMALL, EV_NOTWAIT, EV_GREEN, EV_N };
 constexpr int MAX_CAR_SLOTS = 32;  // the history bit words (AV slots + 4cars followers)
 
 struct Cfg {
@@ -123,6 +128,7 @@ struct Bufs {
   double *envd;   // [N/EB][E_ND][EB]
   int32_t *envi;  // [N/EB][EI_NI][EB]
   uint32_t *mt;   // [N][2][624] (active + next block, see RngT)
+  uint32_t *ev;   // [N/EB][EV_N][EB] event counters (touched only when an event fires)
 };
 
 // Env-blocked state layout: every field array ([rows] per env: car C_NF*nC, ped P_NF*P,
@@ -377,6 +383,7 @@ struct Env {
   MHPPO_HD double &car(int f, int s) const { return b.car[sidx(C_NF * c.nC, f * c.nC + s, e)]; }
   MHPPO_HD double &pedf(int f, int p) const { return b.ped[sidx(P_NF * c.P, f * c.P + p, e)]; }
   MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[sidx(c.P, p, e)]; }
+  MHPPO_HD void event(int k) const { b.ev[sidx(EV_N, k, e)] += 1u; }
 };
 
 #ifdef __HIP__
@@ -536,6 +543,8 @@ struct EnvR {
   MHPPO_HD int32_t &hist_nf(int k) const { return hnf_[k]; }
   MHPPO_HD double &pedf(int f, int p) const { return ped_[f][p]; }
   MHPPO_HD uint32_t &pflag(int p) const { return pfl_[p]; }
+  // events are rare: a lane increments its env's counter in HBM only when one fires
+  MHPPO_HD void event(int k) const { b.ev[sidx(EV_N, k, e)] += 1u; }
 };
 
 struct Ped {
@@ -938,7 +947,10 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
       q.set(F_WSA, worst_delta_l(E, q, Sc, Vc, line) < 0);
     }
     bool cif = is_crossing_in_front(E, q, line, 0);
-    if (ped_accident && (cif && (prev[i] < q.Sx) && (Sc > q.Sx))) q.set(F_ACCIDENT, true);
+    if (ped_accident && (cif && (prev[i] < q.Sx) && (Sc > q.Sx))) {
+      q.set(F_ACCIDENT, true);
+      E.event(EV_ACCIDENT);  // "Accident! : " (:186)
+    }
     if (cif) {
       double dl;
       if ((Vc) < 0.05) dl = (V == V_SCALABLE) ? 100. : 0.;
@@ -946,6 +958,7 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
       double pa;
       if (dl > 0) pa = -1. * exp(-4. * (dl));
       else pa = (V == V_NAIF || V == V_STOP) ? -1. * dl - 1 : 1. * dl - 1;
+      if (pa < -1. && E.car(C_PA, i) >= -1.) E.event(EV_POSSIBLE);  // "Possible accident! " (:199-200)
       E.car(C_PA, i) = pymin(E.car(C_PA, i), pa);
     }
     double Ts = E.car(C_TS, i);
@@ -964,6 +977,13 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
       double ne;
       if (ex) ne = -1. * exp(red ? 4. * (Ts) : -4. * (q.Sx - Sc));
       else ne = red ? -1. * (1 + Ts) : -1. * (1 + Sc - q.Sx);
+      // "Small mistake - priority ? " (:221-222) / "Mauvais signal vert " (:235-236)
+      if (E.car(C_ES, i) >= -1. && ne < -1.) E.event(red ? EV_SMALL : EV_GREEN);
+      // "Pedestrian is not waiting " (:224-227): once per pedestrian (naif: every time, :223-224)
+      if (red && cif && Sc < q.Sx && (V == V_NAIF || !q.has(F_PNW))) {
+        q.set(F_PNW, true);
+        E.event(EV_NOTWAIT);
+      }
       E.car(C_ES, i) = pymin(ne, E.car(C_ES, i));
     }
   }

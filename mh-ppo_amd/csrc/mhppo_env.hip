@@ -73,6 +73,13 @@ __global__ void __launch_bounds__(TPB) k_env_state(Cfg c, Bufs b, double *out, i
   if (e < c.N) env_state_one<V>(c, b, e, out, dim);
 }
 
+__global__ void __launch_bounds__(TPB) k_env_events(Cfg c, Bufs b, uint32_t *out) {
+  const int e = blockIdx.x * TPB + threadIdx.x;
+  if (e < c.N)
+#pragma unroll
+    for (int k = 0; k < EV_N; k++) out[(size_t)e * EV_N + k] = b.ev[sidx(EV_N, k, e)];
+}
+
 __global__ void k_env_rng(Cfg c, Bufs b, uint32_t *mt, int32_t *mti) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   // the active block of each env (the CPython state) and its cursor
@@ -130,8 +137,10 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   size_t bytes_car = sizeof(double) * C_NF * c.nC * N, bytes_ped = sizeof(double) * P_NF * c.P * N;
   size_t bytes_pfl = sizeof(uint32_t) * c.P * N, bytes_envd = sizeof(double) * E_ND * N;
   size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * (MT_BLOCKS * MT_N * (size_t)c.N + MT_PAD);
+  size_t bytes_ev = sizeof(uint32_t) * EV_N * N;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_mt);
+  size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_ev) +
+                 al(bytes_mt);
   if (hipMalloc(&h->blob, total) != hipSuccess) {
     delete h;
     return set_error(MHPPO_ENOMEM, "hipMalloc(%zu) failed", total);
@@ -143,6 +152,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   h->b.pfl = (uint32_t *)p; p += al(bytes_pfl);
   h->b.envd = (double *)p; p += al(bytes_envd);
   h->b.envi = (int32_t *)p; p += al(bytes_envi);
+  h->b.ev = (uint32_t *)p; p += al(bytes_ev);
   h->b.mt = (uint32_t *)p;
   // any failure past the allocation releases the blob and the handle before reporting
   hipError_t e = hipMemset(h->blob, 0, total);
@@ -240,6 +250,15 @@ int mhppo_env_get_state(mhppo_env *env, double *out, void *stream) {
   dim3 grid((env->c.N + TPB - 1) / TPB);
   int dim = mhppo_env_state_dim(env);
   VARIANT_LAUNCH(k_env_state, env->c.variant, grid, (hipStream_t)stream, env->c, env->b, out, dim);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+int mhppo_env_events(mhppo_env *env, uint32_t *out, void *stream) {
+  if (!env || !out) return set_error(MHPPO_EINVAL, "null env/out");
+  GUARD_DEVICE(env->device);
+  dim3 grid((env->c.N + TPB - 1) / TPB);
+  hipLaunchKernelGGL(k_env_events, grid, dim3(TPB), 0, (hipStream_t)stream, env->c, env->b, out);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

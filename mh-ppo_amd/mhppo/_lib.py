@@ -64,6 +64,7 @@ _SIGS = {
     "mhppo_env_step": (I32, [P, P, P, P, P, P, P]),
     "mhppo_env_get_state": (I32, [P, P, P]),
     "mhppo_env_get_rng": (I32, [P, P, P, P]),
+    "mhppo_env_events": (I32, [P, P, P]),
     "mhppo_choice_dim": (I32, [P]),
     "mhppo_rollout_begin": (I32, [P, ctypes.POINTER(Mlp), P, P, ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), P, I32,

@@ -28,6 +28,11 @@ def _flat(x, n):
     return a
 
 
+# the reference env's detection prints, counted per env (include/mhppo.h MHPPO_EV_*)
+EVENT_NAMES = ("Accident! : ", "Possible accident! ", "Small mistake - priority ? ", "Pedestrian is not waiting ",
+               "Mauvais signal vert ")
+
+
 class VecCrosswalk:
     """N independent crosswalk envs of one reference variant on one GPU.
 
@@ -121,6 +126,14 @@ class VecCrosswalk:
         mti = self._t((self.n_envs,), torch.int32)
         _lib.check(_lib.lib().mhppo_env_get_rng(self._h, _lib.ptr(mt), _lib.ptr(mti), _lib.stream_ptr(device=self.device)))
         return mt, mti
+
+    def events(self):
+        """Event counters, int32 [N, 5] (EVENT_NAMES order): how often each of the
+        reference env's detection prints would have fired in every env since its last reset
+        (mhppo_env_events; Env_hybrid_multi_coop_scalable.py:186, 200, 222, 227, 236)."""
+        out = self._t((self.n_envs, len(EVENT_NAMES)), torch.int32)
+        _lib.check(_lib.lib().mhppo_env_events(self._h, _lib.ptr(out), _lib.stream_ptr(device=self.device)))
+        return out
 
     # ------------------------------------------------------------ checkpoint
     def _cfg_key(self):

@@ -117,6 +117,14 @@ class OracleEnv:
         lib().oracle_env_get_rng(self.h, _p(mt), _p(mti))
         return mt, int(mti[0])
 
+    def events(self):
+        """uint32 [5]: detection's print counts since the last reset (env_oracle.c OEnv.events)."""
+        L = lib()
+        L.oracle_env_events.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        out = np.zeros(5, np.uint32)
+        L.oracle_env_events(self.h, _p(out))
+        return out
+
 
 def set_threads(n=0):
     """OpenMP threads of the batch oracle (0 = leave as is); returns the current count."""
@@ -188,6 +196,14 @@ class OracleBatch:
         dm = np.zeros((self.n, self.dump_dim), np.float64)
         L.oracle_batch_dump(self.h, _p(dm))
         return dm
+
+    def events(self):
+        """uint32 [n, 5]: every env's detection print counts since its last reset."""
+        L = lib()
+        L.oracle_batch_events.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        ev = np.zeros((self.n, 5), np.uint32)
+        L.oracle_batch_events(self.h, _p(ev))
+        return ev
 
     def rng_state(self):
         mt = np.zeros((self.n, 624), np.uint32)

@@ -26,6 +26,7 @@ int oracle_env_obs_dim(const OEnv *e);
 void oracle_env_reset(OEnv *e, float *obs);
 int oracle_env_step(OEnv *e, const double *actions, float *obs, double *rewards, double *reward_light);
 int oracle_env_dump(const OEnv *e, double *out);
+void oracle_env_events(const OEnv *e, uint32_t *out);
 int oracle_choice_dim(int variant, int S);
 int oracle_rollout_episode(OEnv *e, int variant, int S, int P, int T, const float *w_cross, const float *w_wait,
                            const float *w_choice, float act_mean, float act_std, const int32_t *forced_a,
@@ -114,6 +115,12 @@ void oracle_batch_step(OBatch *b, const double *actions, float *obs, double *rew
 void oracle_batch_dump(const OBatch *b, double *dump) {
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < b->n; i++) oracle_env_dump(b->e[i], dump + (size_t)i * b->dk);
+}
+
+/* events u32 [n, 5]: every env's detection print counts since its last reset */
+void oracle_batch_events(const OBatch *b, uint32_t *events) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < b->n; i++) oracle_env_events(b->e[i], events + (size_t)i * 5);
 }
 
 /* mt u32 [n, 624], mti i32 [n] */

@@ -87,6 +87,7 @@ typedef struct {
     int sin_model;
     double t_init, T, A, B, w;
     int choose;
+    int ped_not_waiting; /* :35, set at :224-226; only gates its print */
 } Ped;
 
 typedef struct {
@@ -112,6 +113,9 @@ typedef struct {
     int ped_traffic, car_traffic;
     double time, episode_length;
     double reward_light[MAXC];
+    /* detection's prints since reset, counted (Accident!, Possible accident!, Small mistake,
+       Pedestrian is not waiting, Mauvais signal vert: scalable :186,200,222,227,236) */
+    uint32_t events[5];
 } OEnv;
 
 /* ---------------------------------------------------------------- ped -- */
@@ -476,8 +480,10 @@ static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n,
             ped_accident = (!p->accident) * (p->worst_scenario_accident);
             p->worst_scenario_accident = worst_delta_l(e, p, c->Sc, c->Vc, c->line) < 0 ? 1 : 0;
         }
-        if (ped_accident * (is_crossing_in_front(p, c->line, 0) * (prev[i] < p->Sp_x) * (c->Sc > p->Sp_x)))
+        if (ped_accident * (is_crossing_in_front(p, c->line, 0) * (prev[i] < p->Sp_x) * (c->Sc > p->Sp_x))) {
             p->accident = 1;
+            e->events[0]++; /* print("Accident! : ", self.Sp_x) :186 */
+        }
         if (is_crossing_in_front(p, c->line, 0)) {
             double dl;
             if ((c->Vc) < 0.05) dl = (v == V_SCALABLE) ? 100. : 0.;
@@ -485,6 +491,7 @@ static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n,
             double pa;
             if (dl > 0) pa = -1. * exp(-4. * (dl));
             else pa = (v == V_NAIF || v == V_STOP) ? -1. * dl - 1 : 1. * dl - 1;
+            if (pa < -1. && c->possible_accident >= -1.) e->events[1]++; /* "Possible accident! " :199-200 */
             c->possible_accident = pymin(c->possible_accident, pa);
         }
         if (v == V_NAIF) {
@@ -502,12 +509,22 @@ static void ped_detection(OEnv *e, Ped *p, Car *cars, const double *prev, int n,
             double ne;
             if (c->Ts < 0) ne = -1. * exp(4. * (c->Ts));
             else ne = -1. * (1 + c->Ts);
+            if (c->error_scenario >= -1. && ne < -1.) e->events[2]++; /* "Small mistake - priority ? " :221-222 */
+            if (is_crossing_in_front(p, c->line, 0) && (c->Sc < p->Sp_x)) {
+                if (v == V_NAIF) { /* naif :223-224: no flag, printed every time */
+                    e->events[3]++;
+                } else if (!p->ped_not_waiting) { /* :224-227 */
+                    p->ped_not_waiting = 1;
+                    e->events[3]++;
+                }
+            }
             c->error_scenario = pymin(ne, c->error_scenario);
         }
         if (c->light > 0.0) {
             double ne;
             if (p->Sp_x - c->Sc > 0) ne = -1. * exp(-4. * (p->Sp_x - c->Sc));
             else ne = -1. * (1 + c->Sc - p->Sp_x);
+            if (c->error_scenario >= -1. && ne < -1.) e->events[4]++; /* "Mauvais signal vert " :235-236 */
             c->error_scenario = pymin(ne, c->error_scenario);
         }
     }
@@ -615,6 +632,9 @@ void oracle_env_get_rng(const OEnv *e, uint32_t *mt, int32_t *mti) {
     *mti = e->rng.mti;
 }
 
+/* detection's print counts since the last reset, out[5] (include/mhppo.h MHPPO_EV_* order) */
+void oracle_env_events(const OEnv *e, uint32_t *out) { memcpy(out, e->events, sizeof(e->events)); }
+
 int oracle_env_obs_dim(const OEnv *e) {
     switch (e->variant) {
     case V_4CARS:
@@ -677,6 +697,7 @@ void oracle_env_reset(OEnv *e, float *obs) {
     const int v = e->variant;
     e->cross = pyr_uniform(r, e->cross_b[0], e->cross_b[1]);
     e->speed_limit = 10;
+    memset(e->events, 0, sizeof(e->events));
     for (int i = 0; i < e->nb_ped; i++) ped_init(e, &e->peds[i], 0, 0);
     if (v == V_SCALABLE) {
         const int fix = e->flags & 1; /* MHPPO_FIX_SCALABLE_LANES: car(..., i) instead of car(..., i//2) */

@@ -7,6 +7,8 @@ to float64 exactly as the reference rollout passes them (Coop-MH-PPO-scalable.py
 rollout does), random per step, and zeros, so every detection branch runs.
 Run:  python3 tests/golden/gen/make_env_golden.py
 """
+import contextlib
+import io
 import os
 import sys
 
@@ -41,7 +43,17 @@ def n_slots(variant, nb_car, nb_lines):
     return 2 * nb_car if variant == "4cars2" else nb_car
 
 
-def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps):
+EVENTS = ("Accident! : ", "Possible accident! ", "Small mistake - priority ? ", "Pedestrian is not waiting ",
+          "Mauvais signal vert ")  # detection's prints (scalable :186,200,222,227,236), MHPPO_EV_* order
+
+
+def count_events(text):
+    """Per-message counts of the reference env's detection prints in captured stdout."""
+    lines = text.splitlines()
+    return [sum(1 for ln in lines if ln.startswith(m)) for m in EVENTS]
+
+
+def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps, capture_events=False):
     S = n_slots(variant, nb_car, nb_lines)
     arng = np.random.default_rng(seed_base)
     envs, streams = [], []
@@ -56,8 +68,9 @@ def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps):
         mti0.append(streams[e].mti)
     modes = [e % 3 for e in range(n_envs)]  # 0 constant lights, 1 random lights, 2 mixed incl. zeros
     const_light = arng.choice([-1.0, 1.0], size=(n_envs, S))
+    events = []
     for t in range(steps):
-        o_t, r_t, l_t, d_t, m_t, x_t, a_t = [], [], [], [], [], [], []
+        o_t, r_t, l_t, d_t, m_t, x_t, a_t, ev_t = [], [], [], [], [], [], [], []
         for e in range(n_envs):
             acc = arng.uniform(-4.5, 2.5, size=S).astype(np.float32).astype(np.float64)
             if modes[e] == 0:
@@ -67,8 +80,10 @@ def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps):
             else:
                 light = arng.choice([-1.0, 0.0, 1.0], size=S)
             a = np.concatenate([acc, light]).astype(np.float64)
-            with streams[e].active():
+            buf = io.StringIO()
+            with streams[e].active(), contextlib.redirect_stdout(buf):
                 s, r, d, _, _ = envs[e].step(a)
+            ev_t.append(count_events(buf.getvalue()))
             o_t.append(R.flat(s))
             r_t.append(np.asarray(r, dtype=np.float64))
             l_t.append(np.asarray(envs[e].reward_light, dtype=np.float64))
@@ -77,11 +92,12 @@ def run_case(variant, nb_car, nb_ped, nb_lines, n_envs, seed_base, steps):
             x_t.append(R.dump(envs[e]))
             a_t.append(a)
         obs.append(o_t); rew.append(r_t); rl.append(l_t); done.append(d_t); mti.append(m_t)
-        dumps.append(x_t); acts.append(a_t)
+        dumps.append(x_t); acts.append(a_t); events.append(ev_t)
     final_mt = np.array([np.array(st.state[1][:624], dtype=np.uint32) for st in streams])
     sw = lambda x: np.swapaxes(np.array(x), 0, 1)  # [T,E,...] -> [E,T,...]
+    extra = dict(events=sw(events).astype(np.int16)) if capture_events else {}
     return dict(
-        variant=variant, nb_car=nb_car, nb_ped=nb_ped, nb_lines=nb_lines, seed_base=seed_base,
+        **extra, variant=variant, nb_car=nb_car, nb_ped=nb_ped, nb_lines=nb_lines, seed_base=seed_base,
         obs0=np.array(obs0), mti0=np.array(mti0), actions=sw(acts), obs=sw(obs), rewards=sw(rew),
         reward_light=sw(rl), done=sw(done), mti=sw(mti), dump=sw(dumps), final_mt=final_mt,
         final_mti=np.array([st.mti for st in streams]),

@@ -10,7 +10,8 @@ Checked EVERY step for EVERY env, exactly: done, the RNG cursor (number of MT199
 words drawn so far, mod 624 — the data-dependent draw count of the gap-acceptance
 decisions, normalvariate rejections and stop draws), every discrete
 pedestrian field (decision, at_crossing, left, in_cross, accident, time_stop, stop,
-line, need_to_stop, direction, follow_rule), each car's light and existence.  At the
+line, need_to_stop, direction, follow_rule), each car's light and existence, and the five
+per-env event counters (detection's prints, tests/test_events.py).  At the
 end: every env's whole MT19937 state.  Float64 state/rewards: device libm vs glibc may
 differ in the last bits; asserted to rel 1e-9 (float32 observations 1e-6), and the
 fraction of bit-different outputs is reported.
@@ -68,7 +69,8 @@ def test_fullscale_discrete_parity(case):
         ped_o = dm[:, :20 * npd].reshape(N, npd, 20)[:, :, DISCRETE_PED].reshape(N, -1)
         car_g = st[:, 20 * npd:].reshape(N, -1, 8)[:, :, DISCRETE_CAR].reshape(N, -1)
         car_o = dm[:, 20 * npd:].reshape(N, -1, 8)[:, :, DISCRETE_CAR].reshape(N, -1)
-        bad = (d != do) | (mti_g != mti_o) | (ped_g != ped_o).any(1) | (car_g != car_o).any(1)
+        ev_g, ev_o = env.events().cpu().numpy().astype(np.uint32), orc.events()
+        bad = (d != do) | (mti_g != mti_o) | (ped_g != ped_o).any(1) | (car_g != car_o).any(1) | (ev_g != ev_o).any(1)
         first_div[bad & ~div] = t
         div |= bad
         ok = ~div
@@ -95,6 +97,8 @@ def test_fullscale_discrete_parity(case):
                diverged_env_ids=np.nonzero(div)[0][:20].tolist(), float_outputs_bit_different=n_bits,
                float_outputs=n_tot, bit_different_fraction=n_bits / max(n_tot, 1),
                reward_bit_different_fraction=r_bits / max(r_tot, 1),
+               event_counts_gpu=dict(zip(("accident", "possible_accident", "small_mistake", "not_waiting",
+                                          "bad_green"), ev_g.sum(0).tolist())),
                max_rel_err_f64_undiverged=max_rel, max_rel_err_obs_f32_undiverged=max_rel_obs)
     _report(v, rec)
     assert rec["diverged_envs"] == 0 and rec["mt_state_mismatch_envs"] == 0, rec

@@ -31,9 +31,13 @@ def test_gpu_env_matches_reference(path, view):
     env = VecCrosswalk(str(g["variant"]), E, int(g["nb_car"]), npd, int(g["nb_lines"]), seed_base=int(g["seed_base"]),
                        generic_step=view == "generic")
     assert np.array_equal(env.reset().cpu().numpy(), g["obs0"])
+    assert not env.events().any()
+    # detection's prints per env and step, as the reference printed them (tests/test_events.py)
+    ev = np.cumsum(np.load(path.replace("env_", "events_"))["events"], axis=1)
     k = g["dump"].shape[2]
     for t in range(T):
         o, r, rl, d = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        assert np.array_equal(env.events().cpu().numpy(), ev[:, t]), t
         st = env.get_state().cpu().numpy()[:, :k]
         ref = g["dump"][:, t]
         assert np.array_equal(d.cpu().numpy(), g["done"][:, t])

@@ -13,11 +13,12 @@ Discrete, per env, exactly (north_star: "bit-exact discrete action indices / col
 the t = 0 choice actions a_d, the closest pedestrian, car existence, bucket membership (derived),
 every discrete pedestrian / car field of the final env state (decision, at_crossing, left,
 in_cross, accident, time_stop, stop, line, need_to_stop, direction, follow_rule, light,
-exist) and the final MT19937 state + cursor (every data-dependent draw of the episode).  An env
+exist), the episode's per-env event counters (detection's prints: accidents, near misses, ...) and
+the final MT19937 state + cursor (every data-dependent draw of the episode).  An env
 whose rewards move by more than 1e-3 at some step is also counted (an accident or decision
 flip changes a reward by O(1)).  Continuous outputs of the undiverged envs: actions, log-probs,
 features, rewards within the 256-env test's tolerances; bit-different fractions reported.
-Records: gpurun_out/parity_rollout_fullscale_<variant>.json (profiles/r03_parity_rollout/).
+Records: gpurun_out/parity_rollout_fullscale_<variant>.json (profiles/r03_parity_rollout_fullscale/).
 """
 import json
 import os
@@ -88,11 +89,13 @@ def test_policy_rollout_fullscale_parity(case):
     car_g = st[:, 20 * npd:].reshape(N, -1, 8)[:, :, DISCRETE_CAR].reshape(N, -1)
     car_o = dm[:, 20 * npd:].reshape(N, -1, 8)[:, :, DISCRETE_CAR].reshape(N, -1)
     bad_st = (ped_g != ped_o).any(1) | (car_g != car_o).any(1)
+    ev_g = venv.events()  # the episode's detection prints (accident, near miss, ...) per env
+    bad_ev = (ev_g != g(orc.events().astype(np.int32))).any(1)
     rew_g = b.rew  # [N, S, T] f64 view
     rew_o = g(o["rew"])
     rew_jump = ((rew_g - rew_o).abs() > 1e-3)  # an accident / decision flip moves a reward by O(1)
     bad_rw = rew_jump.reshape(N, -1).any(1)
-    div = bad_ad | bad_cl | bad_ex | bad_bk | bad_mt | bad_st | bad_rw
+    div = bad_ad | bad_cl | bad_ex | bad_bk | bad_mt | bad_st | bad_rw | bad_ev
     jt = rew_jump.any(1)  # [N, T]
     first_t = torch.where(jt.any(1), jt.float().argmax(1), torch.full((N,), -1, device=dev))
     ok = ~div
@@ -110,7 +113,10 @@ def test_policy_rollout_fullscale_parity(case):
                diverged_envs=int(div.sum().item()),
                by_check=dict(a_d=int(bad_ad.sum()), closest=int(bad_cl.sum()), exist=int(bad_ex.sum()),
                              bucket=int(bad_bk.sum()), mt_state=int(bad_mt.sum()),
-                             final_discrete_state=int(bad_st.sum()), reward_jump=int(bad_rw.sum())),
+                             final_discrete_state=int(bad_st.sum()), reward_jump=int(bad_rw.sum()),
+                             event_counts=int(bad_ev.sum())),
+               event_counts_gpu=dict(zip(("accident", "possible_accident", "small_mistake", "not_waiting",
+                                          "bad_green"), ev_g.sum(0).tolist())),
                diverged_env_ids=torch.nonzero(div).flatten()[:20].tolist(),
                first_reward_jump_steps=first_t[div][:20].tolist(), continuous_undiverged=cont)
     _report(v, rec)

@@ -26,6 +26,7 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   h->b.pfl = (uint32_t *)calloc((size_t)c.P * N, 4);
   h->b.envd = (double *)calloc((size_t)E_ND * N, 8);
   h->b.envi = (int32_t *)calloc((size_t)EI_NI * N, 4);
+  h->b.ev = (uint32_t *)calloc((size_t)EV_N * N, 4);
   h->b.mt = (uint32_t *)calloc((size_t)MT_BLOCKS * MT_N * c.N + MT_PAD, 4);
   for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
   return h;
@@ -37,6 +38,7 @@ void hs_destroy(HostEnv *h) {
   free(h->b.pfl);
   free(h->b.envd);
   free(h->b.envi);
+  free(h->b.ev);
   free(h->b.mt);
   delete h;
 }
@@ -78,6 +80,10 @@ void hs_step(HostEnv *h, const double *a0, float *obs, double *rew0, double *rl0
 #undef HS_REG
     if (!reg) HS_DISPATCH(env_step_one<V>(h->c, h->b, e, a, obs, rew, rl, done));
   }
+}
+void hs_events(HostEnv *h, uint32_t *out) {
+  for (int e = 0; e < h->c.N; e++)
+    for (int k = 0; k < EV_N; k++) out[(size_t)e * EV_N + k] = h->b.ev[sidx(EV_N, k, e)];
 }
 void hs_state(HostEnv *h, double *out) {
   int dim = hs_state_dim(h);

@@ -21,6 +21,7 @@ L.hs_reset.argtypes = [P, P]
 L.hs_choix.argtypes = [P, P]
 L.hs_step.argtypes = [P, P, P, P, P, P]
 L.hs_state.argtypes = [P, P]
+L.hs_events.argtypes = [P, P]
 
 
 def _p(a):
@@ -67,3 +68,8 @@ class HostVec:
         s = np.zeros((self.N, self.state_dim))
         L.hs_state(self.h, _p(s))
         return s
+
+    def events(self):
+        e = np.zeros((self.N, 5), np.uint32)
+        L.hs_events(self.h, _p(e))
+        return e
