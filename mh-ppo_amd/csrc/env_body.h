@@ -412,7 +412,7 @@ MHPPO_HD void env_step_one(const Cfg &c, const Bufs &b, int e, const double *act
 MHPPO_HD inline void env_seed_one(const Cfg &c, const Bufs &b, int e) {
   uint32_t *blk = b.mt + (size_t)e * (MT_BLOCKS * MT_N);
   rng_seed(blk, c.seed_base + c.env_off + (uint64_t)e);
-  mt_twist_into(blk, blk + MT_N);  // next block ready: active 0, not stale
+  for (int k = 1; k < MT_BLOCKS; k++) mt_twist_into(blk + (k - 1) * MT_N, blk + k * MT_N);  // ring ready
   b.envi[sidx(EI_NI, EI_MTI, e)] = MT_N;
   b.envi[sidx(EI_NI, EI_MTB, e)] = 0;
   b.envd[sidx(E_ND, E_CROSS, e)] = 0.0;

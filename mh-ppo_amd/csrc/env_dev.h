@@ -171,14 +171,20 @@ static constexpr double PI = 0x1.921fb54442d18p+1;
 static constexpr double NV_MAGICCONST = 0x1.b72cd3f331398p+0;  // 4*exp(-0.5)/sqrt(2.0)
 
 // ------------------------------------------------------------ CPython random
-// Each env owns TWO 624-word MT19937 blocks, [N][2][624]: the active block (the
-// CPython state, consumed at cursor mti) and the next block = twist(active), kept
-// ready ahead of time.  Exhausting the active block just switches blocks; the old
-// block is marked stale and regenerated as twist(new active) by the whole wave at
-// the start of the next env kernel (mt_refill_wave: coalesced loads, three LDS
-// phases, coalesced stores), so the 624-step twist never sits on one lane's
-// critical path.  envi[EI_MTB]: bit 0 = active block, bit 1 = the other block is stale.
-enum : int { MT_N = 624, MT_BLOCKS = 2, MT_PAD = 64 };  // MT_PAD: words after the last env's blocks
+// Each env owns a RING of four 624-word MT19937 blocks, [N][4][624]: the active block (the
+// CPython state, consumed at cursor mti) and, ahead of it in ring order, the next three
+// blocks = successive twists of it, kept ready ahead of time.  Exhausting the active block
+// just moves to the next one; the old block is marked stale.  The episode's reset kernel
+// regenerates every stale block (mt_refill_wave: coalesced loads, three LDS phases, coalesced
+// stores, in ring order), so an episode can draw 3 x 624 words beyond its active block — the
+// draw-heavy envs (a pedestrian waiting in front of several cars re-draws its normalvariate
+// gap acceptance every step, up to ~20 words a step) stay within it — and the 624-step twist
+// never sits on one lane's critical path during the rollout; RngT twists in-lane only if an
+// env exhausts the whole ring in one episode.
+// envi[EI_MTB]: bits 0-1 = active block, bit 2 + k = block k is stale.
+enum : int { MT_N = 624, MT_BLOCKS = 4, MT_PAD = 64 };  // MT_PAD: words after the last env's blocks
+MHPPO_HD inline int mt_active(int mtb) { return mtb & 3; }
+MHPPO_HD inline bool mt_stale(int mtb, int k) { return (mtb >> (2 + k)) & 1; }
 
 MHPPO_HD inline uint32_t mt_mix(uint32_t a, uint32_t b) {  // one twist term of (a, successor b)
   uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -208,7 +214,7 @@ struct RngT {
     base = env_blocks;
     mti = mti_;
     mtb = mtb_;
-    mt = base + (mtb & 1) * MT_N;
+    mt = base + mt_active(mtb) * MT_N;
   }
   MHPPO_HD void prefetch() {
     if (K == 0) return;
@@ -220,9 +226,10 @@ struct RngT {
   }
   MHPPO_HD uint32_t genrand() {
     if (mti >= MT_N) {
-      uint32_t *next = base + ((mtb & 1) ^ 1) * MT_N;
-      if (mtb & 2) mt_twist_into(mt, next);  // next block not regenerated yet (>624 draws in one launch)
-      mtb = ((mtb & 1) ^ 1) | 2;             // switch; the old block is now stale
+      const int a = mt_active(mtb), n = (a + 1) & 3;
+      uint32_t *next = base + n * MT_N;
+      if (mt_stale(mtb, n)) mt_twist_into(mt, next);  // ring exhausted within one episode
+      mtb = n | (((mtb >> 2) | (1 << a)) & ~(1 << n)) << 2;  // switch; the old block is now stale
       mt = next;
       mti = 0;
       nwin = 0;
@@ -1048,37 +1055,44 @@ MHPPO_HD inline double car_reward(double Vc) { return -10. * pow_2(Vc - 10.0) / 
 
 #ifdef __HIP__  // HIP translation units (host and device passes), not the host-only simulator
 // Wave-cooperative regeneration of stale MT blocks (see RngT): for every lane of this
-// wave whose next block is stale, the 64 lanes load its active block (coalesced),
-// twist it in three dependency phases through LDS and store the next block.  Call at
-// kernel start from every lane of the wave (valid = this lane owns an env).
+// wave with a stale block, the 64 lanes load its active block (coalesced) and, in ring order,
+// twist each stale block from its predecessor in three dependency phases through LDS (the
+// stale blocks are always a suffix of the ring order after the active one: a block goes
+// stale only when the cursor leaves it), storing each.  Call at kernel start from every lane
+// of the wave (valid = this lane owns an env).
 template <int WAVES>
 __device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool valid) {
-  __shared__ uint32_t sh_src[WAVES][MT_N], sh_dst[WAVES][MT_N];
+  __shared__ uint32_t sh_a[WAVES][MT_N], sh_b[WAVES][MT_N];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int mtb = valid ? b.envi[sidx(EI_NI, EI_MTB, e)] : 0;
-  uint64_t stale = __ballot(valid && (mtb & 2));
+  uint64_t stale = __ballot(valid && (mtb >> 2) != 0);
   if (!stale) return;
-  uint32_t *src = sh_src[w], *dst = sh_dst[w];
   while (stale) {
     const int l = __ffsll((unsigned long long)stale) - 1;
     stale &= stale - 1;
     const int el = __shfl(e, l), bl = __shfl(mtb, l);
     uint32_t *blk = b.mt + (size_t)el * (MT_BLOCKS * MT_N);
-    const uint32_t *g_src = blk + (bl & 1) * MT_N;
-    uint32_t *g_dst = blk + ((bl & 1) ^ 1) * MT_N;
-    for (int k = lane; k < MT_N; k += 64) src[k] = g_src[k];
+    const int a = mt_active(bl);
+    uint32_t *src = sh_a[w], *dst = sh_b[w];
+    int k = 1;
+    while (k < MT_BLOCKS && !mt_stale(bl, (a + k) & 3)) k++;  // first stale block in ring order
+    if (k == MT_BLOCKS) continue;
+    const uint32_t *g_src = blk + ((a + k - 1) & 3) * MT_N;
+    for (int q = lane; q < MT_N; q += 64) src[q] = g_src[q];
+    for (; k < MT_BLOCKS; k++) {
+    uint32_t *g_dst = blk + ((a + k) & 3) * MT_N;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = lane; k < 227; k += 64) dst[k] = src[k + 397] ^ mt_mix(src[k], src[k + 1]);
+    for (int q = lane; q < 227; q += 64) dst[q] = src[q + 397] ^ mt_mix(src[q], src[q + 1]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = 227 + lane; k < 454; k += 64) dst[k] = dst[k - 227] ^ mt_mix(src[k], src[k + 1]);
+    for (int q = 227 + lane; q < 454; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = 454 + lane; k < 623; k += 64) dst[k] = dst[k - 227] ^ mt_mix(src[k], src[k + 1]);
+    for (int q = 454 + lane; q < 623; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1086,8 +1100,12 @@ __device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = lane; k < MT_N; k += 64) g_dst[k] = dst[k];
-    if (lane == l) b.envi[sidx(EI_NI, EI_MTB, el)] = bl & 1;
+    for (int q = lane; q < MT_N; q += 64) g_dst[q] = dst[q];
+    uint32_t *t = src;  // the new block is the next twist's source
+    src = dst;
+    dst = t;
+    }
+    if (lane == l) b.envi[sidx(EI_NI, EI_MTB, el)] = a;  // active block kept, none stale
     // the owning lane reads the new block later in this launch: stores complete first
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

@@ -85,7 +85,7 @@ __global__ void k_env_rng(Cfg c, Bufs b, uint32_t *mt, int32_t *mti) {
   // the active block of each env (the CPython state) and its cursor
   if (i < (size_t)c.N * MT_N) {
     const size_t e = i / MT_N, k = i % MT_N;
-    mt[i] = b.mt[e * (MT_BLOCKS * MT_N) + (b.envi[sidx(EI_NI, EI_MTB, e)] & 1) * MT_N + k];
+    mt[i] = b.mt[e * (MT_BLOCKS * MT_N) + mt_active(b.envi[sidx(EI_NI, EI_MTB, e)]) * MT_N + k];
   }
   if (i < (size_t)c.N) mti[i] = b.envi[sidx(EI_NI, EI_MTI, i)];
 }

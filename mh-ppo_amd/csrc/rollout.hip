@@ -125,15 +125,14 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
 // wave-uniform and stream through the scalar cache as SGPR operands of the FMAs.  (With
 // per-lane heads the weights come from LDS, and 64 lanes reading one weight cost the LDS
 // pipe 64 words: that, not the FMAs, bounds k_policy.)  Same features, same fmaf chains:
-// bit-identical to k_policy.  The waves with 64 gw < N also regenerate the stale MT19937
-// blocks of envs [64 gw, 64 gw + 64) (mt_refill_wave), off the env kernel's critical path.
+// bit-identical to k_policy.  (Stale MT19937 blocks are regenerated once per episode, by the
+// reset kernel: see k_policy_mfma.)
 template <int V>
 __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__restrict__ Wc,
                                                        const float *__restrict__ Ww, float mean_c, float std_c,
                                                        float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
   const int lane = threadIdx.x & 63;
   const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
-  if ((int64_t)gw * 64 < c.N) mt_refill_wave<TPB / 64>(eb, c.N, gw * 64 + lane, gw * 64 + lane < c.N);
   const int R = c.N * c.nS * c.P;
   const int32_t *__restrict__ rows = B.rows;
   const int nc = __builtin_amdgcn_readfirstlane(rows[R]), nw = __builtin_amdgcn_readfirstlane(rows[R + 1]);
@@ -179,7 +178,7 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
 #ifndef MHPPO_POLICY_TPB
 // k_policy_mfma block size: 8 waves share one LDS copy of the two actors, so two blocks per CU
 // give four waves per SIMD (<= 128 VGPRs) to hide the MFMA chains' layer-to-layer latency
-// (LDS per block: 38.7 KB of weights + 39.9 KB of MT-refill images)
+// (LDS per block: 38.7 KB of weights)
 #define MHPPO_POLICY_TPB 512
 #endif
 constexpr int PTPB = MHPPO_POLICY_TPB;
@@ -289,7 +288,12 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
   const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5;
   const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (PTPB / 64) + (tid >> 6)));
   const int nwaves = gridDim.x * (PTPB / 64);
-  if ((int64_t)gw * 64 < c.N) mt_refill_wave<PTPB / 64>(eb, c.N, gw * 64 + l, gw * 64 + l < c.N);
+  // No MT19937 refill here: the episode's reset kernel (k_env_reset) regenerates every stale next
+  // block, so each env starts the episode with a fresh 624-word block in reserve beyond its
+  // active one — more than an episode draws (reset 24-61 words, a step 0-18) — and RngT twists
+  // in-lane in the (correct, never observed) case that an env exhausts both within one episode.
+  // A per-step refill here cost the policy step up to 25 us in the draw-heavy early steps (every
+  // stale env a 624-word twist serialised in its wave) and its first step ~100 us.
   stage_both<PTPB>(lds, Wc, Ww, tid);
   __syncthreads();
   const int R = c.N * c.nS * c.P;
@@ -536,14 +540,13 @@ __global__ void __launch_bounds__(TPB)
   sample_env_body(E, eps, t, B);
 }
 
-// REFILL = false when k_policy_sorted ran just before (it regenerated the stale MT blocks;
-// a block still stale would be twisted in-lane by RngT, so either way the draws are exact)
-template <int V, int NC, int NAV, int NP, bool REFILL>
+// No MT refill in the register-view step kernel: the episode's reset kernel regenerated every stale block
+// (see k_policy_mfma), and a block exhausted twice within one episode is twisted in-lane by RngT
+template <int V, int NC, int NAV, int NP>
 __global__ void __launch_bounds__(TPB)
     k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
   const int e = blockIdx.x * TPB + threadIdx.x;
   MHPPO_MARK(0);
-  if (REFILL) mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
   MHPPO_MARK(1);
   if (e >= c.N) return;
   EnvR<V, NC, NAV, NP> E(c, eb, e);
@@ -972,18 +975,10 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
     if (!use_reg_view(c, V, NC, NAV, NP)) return false;
     const dim3 g = grid_for(c.N);
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (ktime_next(e0, e1)) {  // same launch, with the timing events attached to its dispatch
-      if (B.rows)
-        hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps,
-                              t, B);
-      else
-        hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps, t,
-                              B);
-    } else if (B.rows) {
-      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, false>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
-    } else {
-      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP, true>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
-    }
+    if (ktime_next(e0, e1))  // same launch, with the timing events attached to its dispatch
+      hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps, t, B);
+    else
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
     return true;
   }
 }
@@ -1045,7 +1040,7 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
   size_t R = (size_t)c.N * c.nS * c.P;
   if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
   if (bufs->rows && !(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
-    // persistent 32-row MFMA tiles: 2 blocks per CU, and at least N/64 waves (MT refill)
+    // persistent 32-row MFMA tiles: 2 blocks per CU
     static int cus[mhppo::MAX_DEVICES] = {0};
     const int dev = env_device(env);
     if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
@@ -1055,9 +1050,8 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
       cus[dev] = n;
     }
     constexpr size_t WPB = PTPB / 64;  // waves per block
-    const size_t tiles = R / 32 + 2, waves_env = ((size_t)c.N + 63) / 64;
-    size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + WPB - 1) / WPB);
-    blocks = std::max<size_t>(blocks, (waves_env + WPB - 1) / WPB);
+    const size_t tiles = R / 32 + 2;
+    const size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + WPB - 1) / WPB);
     VLAUNCHB(k_policy_mfma, c.variant, dim3((unsigned)blocks), dim3(PTPB), 2 * pol::HEAD * sizeof(float),
              (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std,
              actor_wait->mean, actor_wait->std, *bufs, env_bufs(env));
@@ -1065,7 +1059,7 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
     return MHPPO_OK;
   }
   if (bufs->rows) {
-    // one wave per 64 rows of one head: at most R/64 + 2 waves, and at least N/64 (MT refill)
+    // one wave per 64 rows of one head: at most R/64 + 2 waves
     const size_t waves = (R + 63) / 64 + 2;
     const dim3 grid((unsigned)((waves + TPB / 64 - 1) / (TPB / 64)));
     VLAUNCH(k_policy_sorted, c.variant, grid, 0, (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed,

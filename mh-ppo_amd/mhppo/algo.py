@@ -74,8 +74,10 @@ class Env_rollout:
             self.batch = self.gpu.collect(actor_net_cross, actor_net_wait, actor_net_choice, seed=self.seed,
                                           iteration=self.iteration, forced_choice=forced_choice, eps_tape=eps_tape)
         self.iteration += 1
-        self.cross, self.wait, self.choice = bucket_segments(self.batch, fix_bucket=self.fix_bucket)
-        self.gpu.check()  # NaN policy outputs raise, as torch.distributions does in the reference
+        # NaN policy outputs raise, as torch.distributions does in the reference: the status word
+        # comes back with the bucket sizes (the iteration's one host sync before the update)
+        self.cross, self.wait, self.choice = bucket_segments(self.batch, fix_bucket=self.fix_bucket,
+                                                             status=self.gpu.status)
         return self.batch
 
     # reference-named views of the collected batch
@@ -158,6 +160,7 @@ class Algo_PPO:
         self.rollout.seed = getattr(self, "seed", 0)
         self.ep_reward_cross, self.ep_reward_wait, self.ep_reward_choice = [], [], []
         self.ep_scenario_balance = []
+        self._pending_curves = []  # (pinned sums, event, m_c, m_w, m_d) not yet appended
         self.last_losses = {}
 
     def nets(self):
@@ -197,12 +200,15 @@ class Algo_PPO:
         dev = self.venv.device
         c, w, d = r.cross, r.wait, r.choice
         with torch.cuda.device(dev):
-            loc = torch.cat([torch.tensor([c["ret"].numel(), w["ret"].numel(), d["ret"].numel()],
-                                          dtype=torch.float64, device=dev),
-                             torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)])
-            ppo._allreduce_(loc)
-            m_c, m_w, m_d = loc[:3].tolist()
-            counts = loc[3:5]
+            counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
+            if ppo._dp():  # global row counts: one all-reduce and one host sync
+                loc = torch.cat([torch.tensor([c["ret"].numel(), w["ret"].numel(), d["ret"].numel()],
+                                              dtype=torch.float64, device=dev), counts])
+                ppo._allreduce_(loc)
+                m_c, m_w, m_d = loc[:3].tolist()
+                counts = loc[3:5]
+            else:  # the local counts are the global ones, known on the host: no sync
+                m_c, m_w, m_d = float(c["ret"].numel()), float(w["ret"].numel()), float(d["ret"].numel())
             heads, names = [], []
             if m_c > 0:  # the reference trains a continuous head only on a non-empty batch (:869, :874)
                 heads.append(ppo.Head("c", self.actor_net_cross, self.critic_net_cross, self.optimizer_actor_cross,
@@ -262,13 +268,15 @@ class Algo_PPO:
             dev = self.venv.device
             sums = torch.stack([rc.double().sum(), rw.double().sum(), rd.double().sum()]).to(dev)
             ppo._allreduce_(sums)
-            sums = sums.tolist()
-            if m_c > 0:  # rew_batch.mean() over the global batch (:886-892)
-                self.ep_reward_cross.append(sums[0] / m_c)
-            if m_w > 0:
-                self.ep_reward_wait.append(sums[1] / m_w)
-            self.ep_reward_choice.append(sums[2] / m_d if m_d > 0 else float("nan"))  # mean() of empty: NaN
-            self.ep_scenario_balance.append([int(m_c), int(m_w)])
+            # the reward curves take the sums without a host sync here: an asynchronous copy to
+            # pinned memory, appended once it has landed (next iteration, or the end of train)
+            host = torch.empty(3, dtype=torch.float64, pin_memory=True)
+            host.copy_(sums, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._pending_curves.append((host, ev, m_c, m_w, m_d))
+            if self.verbose:
+                self._flush_curves()
             if self.verbose and _rank() == 0:
                 print("Episode * {} * And Number of steps is ==> {}".format(ep, ep * self.batch_size))
                 print("Average Cross reward is ==> {}, Average Wait reward is ==> {}".format(
@@ -278,10 +286,28 @@ class Algo_PPO:
                 print("Number Cross is ==> {} and Number Wait is ==> {} ".format(int(m_c), int(m_w)))
             self.rollout.reset()
             self.total_loop = self.total_loop + 1
+            if len(self._pending_curves) > 1:  # the previous iteration's sums landed long ago
+                self._flush_curves(keep_last=True)
+        self._flush_curves()
         if _rank() == 0 and self.save_curves:
             self.save_reward_curves()
         if self.verbose and _rank() == 0:
             print("Complete")
+
+    def _flush_curves(self, keep_last=False):
+        """Append the reward-curve entries (rew_batch.mean() over the global batch, :886-892) of
+        the iterations whose reward sums have been read back."""
+        n = len(self._pending_curves) - (1 if keep_last else 0)
+        for host, ev, m_c, m_w, m_d in self._pending_curves[:n]:
+            ev.synchronize()
+            s = host.tolist()
+            if m_c > 0:
+                self.ep_reward_cross.append(s[0] / m_c)
+            if m_w > 0:
+                self.ep_reward_wait.append(s[1] / m_w)
+            self.ep_reward_choice.append(s[2] / m_d if m_d > 0 else float("nan"))  # mean() of empty: NaN
+            self.ep_scenario_balance.append([int(m_c), int(m_w)])
+        del self._pending_curves[:n]
 
     def _curve_path(self, name):
         pre = PREFIX.get(self.venv.variant, "pappo")

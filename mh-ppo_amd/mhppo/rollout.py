@@ -190,7 +190,20 @@ def returns_scan(rew, gamma=0.99):
     return out.reshape(rew.shape)
 
 
-def bucket_segments(batch, fix_bucket=False):
+NAN_STATUS_MSG = {1: "Categorical probs of the choice actor, :409",
+                  2: "MultivariateNormal loc of the continuous actors, :451"}
+
+
+def raise_if_nan_status(st):
+    """The host side of mhppo_rollout_check for a status word already read back: raise
+    MhppoNaNError (a ValueError, as the reference's torch.distributions raise) when set."""
+    st = int(st)
+    if st:
+        what = "; ".join(m for b, m in NAN_STATUS_MSG.items() if st & b)
+        raise _lib.MhppoNaNError(f"NaN policy output sampled ({what}): the reference raises ValueError here")
+
+
+def bucket_segments(batch, fix_bucket=False, status=None):
     """Split (env, slot) episode segments into the reference's cross/wait/choice batches.
     fix_bucket=True (opt-in bug fix) buckets car i by ITS closest
     pedestrian's decision action_d[i*P + closest_i] instead of the flat action_d[i].
@@ -199,6 +212,11 @@ def bucket_segments(batch, fix_bucket=False):
     action_d[i] <= 0 where action_d is the per-(car, ped) array indexed by the CAR
     index i.  Choice sample per existing car: the closest pedestrian's
     features, action and log-prob, reward = episodic min of reward_light.
+
+    One host synchronisation: the three bucket sizes (and, when `status` -- the rollout's
+    NaN-flag word, int32 [1] on the device -- is given, that word, raised on as
+    RolloutGPU.check would) come back in one read; the segment lists are then built with
+    nonzero_static at the known sizes.
     """
     N, S, P, T = batch.N, batch.S, batch.P, batch.T
     a_flat = batch.a_d.reshape(N, S * P)
@@ -207,12 +225,21 @@ def bucket_segments(batch, fix_bucket=False):
         action_d_i = 2 * a_car.to(torch.int32) - 1
     else:
         action_d_i = 2 * a_flat[:, :S].to(torch.int32) - 1  # action_d[i], i < S
-    exist = batch.exist.bool()
-    cross = exist & (action_d_i <= 0)
-    wait = exist & (action_d_i > 0)
-    seg_cross = torch.nonzero(cross.reshape(-1)).squeeze(1)
-    seg_wait = torch.nonzero(wait.reshape(-1)).squeeze(1)
-    seg_all = torch.nonzero(exist.reshape(-1)).squeeze(1)
+    exist = batch.exist.bool().reshape(-1)
+    cross = exist & (action_d_i <= 0).reshape(-1)
+    wait = exist & (action_d_i > 0).reshape(-1)
+    sizes = [cross.sum(), wait.sum(), exist.sum()]
+    if status is not None:
+        sizes.append(status.reshape(-1)[0].to(torch.int64))
+    sizes = torch.stack(sizes).tolist()
+    if status is not None:
+        if sizes[3]:
+            status.zero_()
+        raise_if_nan_status(sizes[3])
+    n_cross, n_wait, n_all = sizes[:3]
+    seg_cross = torch.nonzero_static(cross, size=n_cross).squeeze(1)
+    seg_wait = torch.nonzero_static(wait, size=n_wait).squeeze(1)
+    seg_all = torch.nonzero_static(exist, size=n_all).squeeze(1)
     ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
 
     cross_r, wait_r = scatter_buckets(seg_cross, seg_wait, N * S, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm,
@@ -226,7 +253,7 @@ def bucket_segments(batch, fix_bucket=False):
         act=batch.a_d.reshape(-1).index_select(0, base),
         logp=batch.logp_d.reshape(-1).index_select(0, base),
         ret=batch.ep_min.reshape(-1).index_select(0, seg_all).float(),
-        n_seg=int(seg_all.numel()),
+        n_seg=n_all,
     )
     return cross_r, wait_r, choice
 
