@@ -756,8 +756,8 @@ constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
 constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
 // per-wave slot: the tile image (also the f32 transpose image), two input slots (double
-// buffered), the float64 loss sums
-constexpr int O_IN = (IMG + 15) / 16 * 16, O_DACC = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_DACC + 96 * 8;
+// buffered)
+constexpr int O_IN = (IMG + 15) / 16 * 16, WAVE_B = O_IN + 2 * LY::IN_SZ * 4;
 constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -1053,8 +1053,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   // bias-gradient row sums (lane j, half kh: the half-tile sums of feature j)
   float gsum[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // gB2a gB2b gB3 gW4 gB4
   auto radd = [&](int k, float v) { gsum[k] += v; };
-  double *dacc = reinterpret_cast<double *>(wb + O_DACC) + j;
-  if (kh == 0) dacc[0] = dacc[32] = dacc[64] = 0.0;
+  // float64 loss / advantage sums in registers (lanes kh == 0), folded once after the loop: an
+  // LDS read-modify-write per tile put its latency on the loss section's serial chain (-1 %)
+  double dsum0 = 0.0, dsum1 = 0.0, dsum2 = 0.0;
   float meanf = 0.f, stdf = 1.f;
   if (KIND != K_CRITIC) {
     double mean = stats[0] / m_global;
@@ -1135,9 +1136,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
         const float a = rt - v;
         const float d = v - rt;
         if (kh == 0) {
-          dacc[0] += (double)d * (double)d;
-          dacc[32] += (double)a;
-          dacc[64] += (double)a * (double)a;
+          dsum0 += (double)d * (double)d;
+          dsum1 += (double)a;
+          dsum2 += (double)a * (double)a;
         }
         dy0 = (float)(2.0 * inv_m * (double)d);
       } else {
@@ -1151,7 +1152,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
         const double r = exp((double)lp - (double)slot[LY::IN_S1 + 32 + j]);
         double dfdr;
         const double f = surr_and_grad(r, (double)A, dfdr);
-        if (kh == 0) dacc[0] += f;
+        if (kh == 0) dsum0 += f;
         const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
         dy0 = (dmu * out_std) * (1.0f - t * t);
       }
@@ -1291,7 +1292,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  if (kh == 0) s0 = dacc[0], s1 = dacc[32], s2 = dacc[64];
+  if (kh == 0) s0 = dsum0, s1 = dsum1, s2 = dsum2;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s0 += __shfl_xor(s0, o);
