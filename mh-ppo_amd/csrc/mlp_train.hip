@@ -756,8 +756,8 @@ constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
 constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
 // per-wave slot: the tile image (also the f32 transpose image), two input slots (double
-// buffered)
-constexpr int O_IN = (IMG + 15) / 16 * 16, WAVE_B = O_IN + 2 * LY::IN_SZ * 4;
+// buffered), a second tile image
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
 constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -845,6 +845,46 @@ __device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
 __device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6("v_mfma_f32_32x32x16_bf16"); }
 __device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6("v_mfma_f32_16x16x32_bf16"); }
 #undef X3_MACC6
+// C += A B (six products, as macc6) with the next fragment's six transposed image reads issued
+// in the MFMA gaps (an LDS read between two 32x32x16 MFMAs costs the wave almost nothing, a run
+// of them costs their issue and puts their latency in front of the MFMAs that need them).  The
+// compiler does not see these reads: WAIT puts an lgkmcnt(0) in front of a block whose B
+// fragment came from the previous block's reads (LDS returns in order, so the compiler's own
+// counted waits stay sufficient with them in flight).  nx <- image K-step rows at rbase + off.
+#define X3_MACC6_RD(NAME, ACC, OP)                                                                          \
+  template <bool WAIT, int OFF>                                                                              \
+  __device__ __forceinline__ void NAME(const F3 &a, const F3 &b, ACC &c, F3 &nx, const char *rbase) {       \
+    constexpr int U = 4 * IM_ROWB;                                                                           \
+    const uint32_t ad = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)rbase;         \
+    uint2 r0, r1, r2, r3, r4, r5;                                                                            \
+    if constexpr (WAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
+    asm volatile("s_nop 1\n\t" OP " %0, %9, %10, %0\n\tds_read_b64_tr_b16 %1, %13 offset:%14\n\t" OP          \
+                 " %0, %7, %12, %0\n\tds_read_b64_tr_b16 %2, %13 offset:%15\n\t" OP                           \
+                 " %0, %8, %11, %0\n\tds_read_b64_tr_b16 %3, %13 offset:%16\n\t" OP                           \
+                 " %0, %8, %10, %0\n\tds_read_b64_tr_b16 %4, %13 offset:%17\n\t" OP                           \
+                 " %0, %7, %11, %0\n\tds_read_b64_tr_b16 %5, %13 offset:%18\n\t" OP                           \
+                 " %0, %7, %10, %0\n\tds_read_b64_tr_b16 %6, %13 offset:%19"                                 \
+                 : "+a"(c), "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5)                 \
+                 : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2]), "v"(ad),    \
+                   "i"(OFF), "i"(OFF + U), "i"(OFF + IM_PART), "i"(OFF + IM_PART + U), "i"(OFF + 2 * IM_PART), \
+                   "i"(OFF + 2 * IM_PART + U)                                                                \
+                 : "memory");                                                                                \
+    nx.p[0] = u32x4{r0.x, r0.y, r1.x, r1.y};                                                                  \
+    nx.p[1] = u32x4{r2.x, r2.y, r3.x, r3.y};                                                                  \
+    nx.p[2] = u32x4{r4.x, r4.y, r5.x, r5.y};                                                                  \
+  }
+X3_MACC6_RD(macc6_rd, f32x16, "v_mfma_f32_32x32x16_bf16")
+X3_MACC6_RD(macc6_16_rd, f32x4, "v_mfma_f32_16x16x32_bf16")
+#undef X3_MACC6_RD
+// the last block of a chain: wait for its asm-read fragment, then the six MFMAs
+__device__ __forceinline__ void macc6_w(const F3 &a, const F3 &b, f32x16 &c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  macc6(a, b, c);
+}
+__device__ __forceinline__ void macc6_16_w(const F3 &a, const F3 &b, f32x4 &c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  macc6_16(a, b, c);
+}
 // before the accumulators are read: the last MFMA's result latency (>= 18 passes)
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
@@ -1180,15 +1220,21 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     lds_order();
     const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
     lds_order();
-    img_write(imw, split_step(h2a, 0), split_step(h2a, 1));
+    // h2a to the second image, h2b behind the d3 reads in the first: every later fragment is
+    // read in the gaps of the MFMA block before the one that consumes it
+    img_write(imw + O_IM2, split_step(h2a, 0), split_step(h2a, 1));
     lds_order();
-    macc6(ad0, img_read(imr, 0), gW3a);
-    macc6(ad1, img_read(imr, 1), gW3a);
+    const F3 ha0 = img_read(imr + O_IM2, 0);
     lds_order();
     img_write(imw, split_step(h2b, 0), split_step(h2b, 1));
     lds_order();
-    macc6(ad0, img_read(imr, 0), gW3b);
-    macc6(ad1, img_read(imr, 1), gW3b);
+    {
+      F3 ha1, hb0, hb1;
+      macc6_rd<false, O_IM2 + 16 * IM_ROWB>(ad0, ha0, gW3a, ha1, imr);
+      macc6_rd<true, 0>(ad1, ha1, gW3a, hb0, imr);
+      macc6_rd<true, 16 * IM_ROWB>(ad0, hb0, gW3b, hb1, imr);
+      macc6_w(ad1, hb1, gW3b);
+    }
     lds_order();
     x3_phase();
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
@@ -1210,7 +1256,34 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     x3_phase();
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
     f32x16 d1 = zero16();
-    {
+    if constexpr (KIND != K_CRITIC) {
+      const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
+      d1 = mfma6(bw2(0), f0, d1);
+      d1 = mfma6(bw2(1), f1, d1);
+      // B = h1 image (second slot), A = d2a image (first slot), then d2b into the second slot
+      // behind the h1 reads; the A fragments after the first are read in the MFMA gaps
+      img_write(imw + O_IM2, split_step(h1, 0), split_step(h1, 1));
+      lds_order();
+      const F3 bh0 = img_read(imr + O_IM2, 0), bh1 = img_read(imr + O_IM2, 1);
+      lds_order();
+      img_write(imw, f0, f1);
+      lds_order();
+      const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
+      img_write(imw + O_IM2, f2, f3);
+      lds_order();
+      d1 = mfma6(bw2(2), f2, d1);
+      d1 = mfma6(bw2(3), f3, d1);
+      const F3 da0 = img_read(imr, 0);
+      lds_order();
+      {
+        F3 da1, db0, db1;
+        macc6_rd<false, 16 * IM_ROWB>(da0, bh0, gW2a, da1, imr);
+        macc6_rd<true, O_IM2>(da1, bh1, gW2a, db0, imr);
+        macc6_rd<true, O_IM2 + 16 * IM_ROWB>(db0, bh0, gW2b, db1, imr);
+        macc6_w(db1, bh1, gW2b);
+      }
+      lds_order();
+    } else {  // (the critic pass holds its forward weight fragments: no registers for the reads ahead)
       const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
       d1 = mfma6(bw2(0), f0, d1);
       d1 = mfma6(bw2(1), f1, d1);
@@ -1250,8 +1323,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
         xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
       }
       const F3 b = split8(xv);
-      macc6_16(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0]);
-      macc6_16(tr_pair<IM_PART>(imr16 + 32, 4 * IM_ROWB), b, gW1t[1]);
+      F3 a1;
+      macc6_16_rd<false, 32>(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0], a1, imr16);
+      macc6_16_w(a1, b, gW1t[1]);
     }
     lds_order();
     x3_phase();

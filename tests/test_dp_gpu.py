@@ -50,3 +50,21 @@ def test_bench_launches_two_ranks(tmp_path):
     a, b = np.load(one), np.load(two)
     assert np.isfinite(a).all()
     np.testing.assert_allclose(b, a, rtol=0, atol=1e-5)
+
+
+def test_rccl_collectives_one_rank(tmp_path):
+    """The update's RCCL path (backend "nccl", device-bound init, the advantage-sum / gradient-
+    bucket / count all-reduces on device tensors) exercised on the one-GPU box: one rank with the
+    collectives forced on trains the same nets as the plain process (a one-rank SUM is the
+    identity; 1e-6 absolute leaves room only for a summation-order difference)."""
+    one, rc = str(tmp_path / "one.npy"), str(tmp_path / "rccl.npy")
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    subprocess.run([sys.executable, WORKER, "--envs-total", "1024", "--out", one], check=True, timeout=240,
+                   env=env, cwd=tmp_path)
+    subprocess.run([sys.executable, WORKER, "--envs-total", "1024", "--out", rc, "--nccl-world1"], check=True,
+                   timeout=240, env=env, cwd=tmp_path)
+    a, b = np.load(one), np.load(rc)
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)
