@@ -1108,6 +1108,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
 
   int cb = 0;
+  MHPPO_MARK(0);
   if (gw < nfull) prefetch_tile<KIND, LY>(inb, X, ret, V, act, lp_old, gw * 32, l);
   for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
     const int64_t row0 = tile * 32;
@@ -1123,6 +1124,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
       load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
     }
     wave_sync();  // the tile's inputs have landed
+    MHPPO_MARK(1);  // timing builds: the tile-input wait
     const float *Xs = slot + LY::IN_X;
     // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
     auto layer1 = [&]() {
@@ -1141,6 +1143,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     };
     f32x16 h1 = layer1();
     x3_phase();
+    MHPPO_MARK(2);
     // ---- layer 2 (the biases ride in as the chains' initial accumulators)
     f32x16 h2a = feat_vec(F, kh), h2b = feat_vec(F + 32, kh);
 #pragma unroll
@@ -1152,6 +1155,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     relu16(h2a);
     relu16(h2b);
     x3_phase();
+    MHPPO_MARK(3);
     // ---- layer 3
     f32x16 h3 = feat_vec(F + 64, kh);
 #pragma unroll
@@ -1160,6 +1164,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     for (int s = 0; s < 2; s++) h3 = mfma6(fw3(2 + s), split_step(h2b, s), h3);
     relu16(h3);
     x3_phase();
+    MHPPO_MARK(4);
     // ---- output and loss gradient dL/dy for this lane's row (as the f32 path)
     const f32x16 w4v = feat_vec(F + 96, kh);
     float part0 = 0.0f;
@@ -1214,6 +1219,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     radd(2, half_row_sum(T, l));
     lds_order();
     x3_phase();
+    MHPPO_MARK(5);
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
     const F3 d3f0 = split_step(d3, 0), d3f1 = split_step(d3, 1);
     img_write(imw, d3f0, d3f1);
@@ -1237,6 +1243,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     }
     lds_order();
     x3_phase();
+    MHPPO_MARK(6);
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
     f32x16 d2a = zero16(), d2b = zero16();
     d2a = mfma6(bw3(0, 0), d3f0, d2a);
@@ -1254,6 +1261,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     radd(1, half_row_sum(T, l));
     lds_order();
     x3_phase();
+    MHPPO_MARK(7);
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
     f32x16 d1 = zero16();
     if constexpr (KIND != K_CRITIC) {
@@ -1308,6 +1316,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     }
     relu_mask(d1, h1);
     x3_phase();
+    MHPPO_MARK(8);
     // ---- dW1 = sum over rows of d1 (x) [X | 1]: A = d1 image, B = the input rows (column 13:
     // the constant 1, i.e. dB1).  16x16x32 tiles (out features 16t..16t+15 x input columns
     // 0..15, all 32 rows in one K-step): lane l of group G = l >> 4 holds rows 8G..8G+7 of
@@ -1329,8 +1338,10 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     }
     lds_order();
     x3_phase();
+    MHPPO_MARK(9);
   }
   // ---- write this wave's partial gradient (packed torch layout)
+  MHPPO_MARK_FLUSH();
   macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
   float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
   float *gp = gpart + (size_t)gw * NWP;

@@ -359,9 +359,11 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
     float y = 0.0f;
 #pragma unroll
     for (int s = 0; s < 16; s++) {
-      const float own = h3[s], oth = __shfl_xor(own, 32);
-      y = fmaf(Wl[O_W4 + 2 * s], kh ? oth : own, y);
-      y = fmaf(Wl[O_W4 + 2 * s + 1], kh ? own : oth, y);
+      // neuron 2s sits in register s of the lower lane half, 2s + 1 in the upper: one
+      // v_permlane32_swap gives every lane both (r[0] = neuron 2s, r[1] = neuron 2s + 1 of its row)
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(h3[s]), __float_as_uint(h3[s]), false, false);
+      y = fmaf(Wl[O_W4 + 2 * s], __uint_as_float(r[0]), y);
+      y = fmaf(Wl[O_W4 + 2 * s + 1], __uint_as_float(r[1]), y);
     }
     const float out = y + Wl[O_B4];
     if (valid && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)

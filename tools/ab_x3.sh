@@ -7,6 +7,9 @@ for v in "$@"; do
   if [ "$v" = base ]; then lib=""; else lib="build_ab/$v/libmhppo.so"; fi
   echo "== $v split"
   MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 || exit 1
-  [ -n "$AB_EXACT" ] && echo "== $v exact f32"
-  [ -n "$AB_EXACT" ] && { MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 --exact || exit 1; }
+  if [ -n "$AB_EXACT" ]; then
+    echo "== $v exact f32"
+    MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 --exact || exit 1
+  fi
 done
+exit 0
