@@ -716,8 +716,12 @@ constexpr int SEGS = 64, STEPS = 16;
 // segments per instruction, and unpadded strides (208 / 16 words) put those 64 lanes on 4
 // banks (16-way conflicts on every record field)
 constexpr int OBS_SEG = STEPS * NF_C + 1, V_SEG = STEPS + 1;
+#ifndef MHPPO_BK_TPB
+#define MHPPO_BK_TPB 1024  // 16 waves: two blocks (75 KB of LDS each) fill a CU
+#endif
+constexpr int BTPB = MHPPO_BK_TPB;
 }
-__global__ void __launch_bounds__(TPB)
+__global__ void __launch_bounds__(bk::BTPB)
     k_bucket_scatter(const int64_t *__restrict__ pos, const int8_t *__restrict__ bucket, int64_t NS, int T,
                      const float *__restrict__ obs, const float *__restrict__ act, const float *__restrict__ logp,
                      const float *__restrict__ ret, const double *__restrict__ rew, mhppo_bucket_dst d0,
@@ -737,23 +741,40 @@ __global__ void __launch_bounds__(TPB)
     s_b[tid] = tid < nseg ? bucket[s0 + tid] : 0;
   }
   __syncthreads();
-  for (int i = tid; i < SEGS * STEPS; i += TPB) {  // i = step * SEGS + seg: lanes on consecutive segments
+  // the observation records of one step of the block's 64 segments are 64 x 13 consecutive
+  // floats: lanes read them as one flat run (every load instruction on two 128-byte lines), all
+  // of a lane's loads issued before its first LDS store
+  {
+    constexpr int NQ = SEGS * NF_C * STEPS / BTPB;
+    static_assert(SEGS * NF_C * STEPS % BTPB == 0, "bucket scatter: block size");
+    float v[NQ];
+    int at[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int i = tid + q * BTPB, tl = i / (SEGS * NF_C), k = i - tl * (SEGS * NF_C), sg = k / NF_C;
+      const bool in = sg < nseg && tl < nt;  // (in-range loads are unconditional: no branches)
+      at[q] = in && s_pos[sg] >= 0 ? sg * OBS_SEG + tl * NF_C + (k - sg * NF_C) : -1;
+      v[q] = obs[in ? ((int64_t)(t0 + tl) * NS + s0) * NF_C + k : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      if (at[q] >= 0) s_obs[at[q]] = v[q];
+  }
+#pragma unroll
+  for (int i = tid; i < SEGS * STEPS; i += BTPB) {  // i = step * SEGS + seg: lanes on consecutive segments
     const int sg = i % SEGS, tl = i / SEGS;
     if (sg >= nseg || tl >= nt || s_pos[sg] < 0) continue;
     const int64_t rec = (int64_t)(t0 + tl) * NS + s0 + sg;
     const int o = sg * V_SEG + tl;  // LDS: segment-major
-    const float *so = obs + rec * NF_C;
-#pragma unroll
-    for (int j = 0; j < NF_C; j++) s_obs[sg * OBS_SEG + tl * NF_C + j] = so[j];
     s_v[0][o] = act[rec];
     s_v[1][o] = logp[rec];
     s_v[2][o] = ret[rec];
     s_rew[o] = rew[rec];
   }
   __syncthreads();
-  // each wave writes the runs of 16 segments: segment sg's rows pos*T + t0 .. + nt
+  // the waves take the segments in turn: segment sg's rows pos*T + t0 .. + nt leave as one run
   const int w = tid >> 6, l = tid & 63;
-  for (int sg = w; sg < nseg; sg += TPB / 64) {
+  for (int sg = w; sg < nseg; sg += BTPB / 64) {
     const int64_t p = s_pos[sg];
     if (p < 0) continue;
     const mhppo_bucket_dst &D = s_b[sg] ? d1 : d0;
@@ -1231,7 +1252,7 @@ int mhppo_bucket_scatter(const int64_t *pos, const int8_t *bucket, int64_t NS, i
   const int64_t nb = (NS + bk::SEGS - 1) / bk::SEGS;
   if (nb > 0x7fffffff) return set_error(MHPPO_EINVAL, "too many segments");
   dim3 g((unsigned)nb, (unsigned)((T + bk::STEPS - 1) / bk::STEPS));
-  hipLaunchKernelGGL(k_bucket_scatter, g, dim3(TPB), 0, (hipStream_t)stream, pos, bucket, NS, (int)T, obs_tm,
+  hipLaunchKernelGGL(k_bucket_scatter, g, dim3(bk::BTPB), 0, (hipStream_t)stream, pos, bucket, NS, (int)T, obs_tm,
                      act_tm, logp_tm, ret_tm, rew_tm, dst[0], dst[1]);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
