@@ -340,7 +340,13 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
     }
     f32x16 h1 = zero16();
 #pragma unroll
-    for (int s = 0; s < 7; s++) h1 = mfma(Wl[O_W1 + j * S1 + 2 * s + kh], kh ? f[2 * s + 1] : f[2 * s], h1);
+    for (int s = 0; s < 7; s++) {
+      // both lane halves hold the row's features: the lower half takes f[2s], the upper f[2s + 1]
+      // (one v_permlane32_swap; a lane-select of the two is folded into an indexed load of f,
+      // which puts f in scratch memory)
+      const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(f[2 * s]), __float_as_uint(f[2 * s + 1]), false, false);
+      h1 = mfma(Wl[O_W1 + j * S1 + 2 * s + kh], __uint_as_float(x[0]), h1);
+    }
     bias_relu(h1, Wl + O_B1, kh);
     f32x16 h2a = zero16(), h2b = zero16();
 #pragma unroll
