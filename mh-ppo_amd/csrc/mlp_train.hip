@@ -837,11 +837,12 @@ __device__ __forceinline__ f32x4 mfma6_16(const F3 &a, const F3 &b, f32x4 c) {
 // between the register files and the arch VGPRs stay free for the tile's values.  Written as
 // one asm block: "s_nop 1" covers the VALU-write -> MFMA-read hazard on A / B (the compiler
 // cannot see the MFMAs inside), and back-to-back accumulation into the same AGPRs needs none.
-#define X3_MACC6(OP)                                                                                 \
-  asm("s_nop 1\n\t" OP " %0, %3, %4, %0\n\t" OP " %0, %1, %6, %0\n\t" OP " %0, %2, %5, %0\n\t" OP  \
-      " %0, %2, %4, %0\n\t" OP " %0, %1, %5, %0\n\t" OP " %0, %1, %4, %0"                              \
-      : "+a"(c)                                                                                      \
-      : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2]))
+#define X3_MACC6_BODY(OP)                                                                                \
+  "s_nop 1\n\t" OP " %0, %3, %4, %0\n\t" OP " %0, %1, %6, %0\n\t" OP " %0, %2, %5, %0\n\t" OP " %0, %2, %4, %0\n\t" OP \
+  " %0, %1, %5, %0\n\t" OP " %0, %1, %4, %0"                                                                      \
+      : "+a"(c)                                                                                                      \
+      : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b.p[0]), "v"(b.p[1]), "v"(b.p[2])
+#define X3_MACC6(OP) asm(X3_MACC6_BODY(OP))
 __device__ __forceinline__ void macc6(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6("v_mfma_f32_32x32x16_bf16"); }
 __device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6("v_mfma_f32_16x16x32_bf16"); }
 #undef X3_MACC6
@@ -876,15 +877,15 @@ __device__ __forceinline__ void macc6_16(const F3 &a, const F3 &b, f32x4 &c) { X
 X3_MACC6_RD(macc6_rd, f32x16, "v_mfma_f32_32x32x16_bf16")
 X3_MACC6_RD(macc6_16_rd, f32x4, "v_mfma_f32_16x16x32_bf16")
 #undef X3_MACC6_RD
-// the last block of a chain: wait for its asm-read fragment, then the six MFMAs
-__device__ __forceinline__ void macc6_w(const F3 &a, const F3 &b, f32x16 &c) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  macc6(a, b, c);
-}
-__device__ __forceinline__ void macc6_16_w(const F3 &a, const F3 &b, f32x4 &c) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  macc6_16(a, b, c);
-}
+// the last block of a chain: wait for its asm-read fragment, then the six MFMAs — ONE volatile
+// statement: as two, the compiler may hoist the (non-volatile) MFMA block above the wait, and the
+// MFMAs then read registers whose LDS data is still in flight (tools/check_asm_rd.py found
+// exactly that in the actor's last dW3 block before this was one statement)
+#define X3_MACC6_W(OP) asm volatile("s_waitcnt lgkmcnt(0)\n\t" X3_MACC6_BODY(OP) : "memory")
+__device__ __forceinline__ void macc6_w(const F3 &a, const F3 &b, f32x16 &c) { X3_MACC6_W("v_mfma_f32_32x32x16_bf16"); }
+__device__ __forceinline__ void macc6_16_w(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6_W("v_mfma_f32_16x16x32_bf16"); }
+#undef X3_MACC6_W
+#undef X3_MACC6_BODY
 // before the accumulators are read: the last MFMA's result latency (>= 18 passes)
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));

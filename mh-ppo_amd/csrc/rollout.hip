@@ -288,10 +288,11 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
   const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5;
   const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (PTPB / 64) + (tid >> 6)));
   const int nwaves = gridDim.x * (PTPB / 64);
-  // No MT19937 refill here: the episode's reset kernel (k_env_reset) regenerates every stale next
-  // block, so each env starts the episode with a fresh 624-word block in reserve beyond its
-  // active one — more than an episode draws (reset 24-61 words, a step 0-18) — and RngT twists
-  // in-lane in the (correct, never observed) case that an env exhausts both within one episode.
+  // No MT19937 refill here: the episode's reset kernel (k_env_reset) regenerates every stale block
+  // of each env's 4-block ring (env_dev.h, MT_BLOCKS), so each env starts the episode with three
+  // fresh 624-word blocks in reserve beyond its active one — more than an episode draws (reset
+  // 24-61 words, a step 0-18) — and RngT twists in-lane in the (correct, never observed) case
+  // that an env exhausts the whole ring within one episode.
   // A per-step refill here cost the policy step up to 25 us in the draw-heavy early steps (every
   // stale env a 624-word twist serialised in its wave) and its first step ~100 us.
   stage_both<PTPB>(lds, Wc, Ww, tid);

@@ -158,6 +158,9 @@ class Algo_PPO:
         self.cov_mat_d = torch.diag(self.cov_var_d)
         self.rollout = Env_rollout(venv, S, self.max_steps, self.dt)
         self.rollout.seed = getattr(self, "seed", 0)
+        # reward curves (:886-892).  While train() runs with verbose=False they lag by one
+        # iteration: an iteration's sums are read back asynchronously and appended at the next
+        # iteration (or at the end of train()); curves() / save_checkpoint() flush them first.
         self.ep_reward_cross, self.ep_reward_wait, self.ep_reward_choice = [], [], []
         self.ep_scenario_balance = []
         self._pending_curves = []  # (pinned sums, event, m_c, m_w, m_d) not yet appended
@@ -309,6 +312,11 @@ class Algo_PPO:
             self.ep_scenario_balance.append([int(m_c), int(m_w)])
         del self._pending_curves[:n]
 
+    def curves(self):
+        """The reward curves with every pending entry appended: (cross, wait, choice, balance)."""
+        self._flush_curves()
+        return self.ep_reward_cross, self.ep_reward_wait, self.ep_reward_choice, self.ep_scenario_balance
+
     def _curve_path(self, name):
         pre = PREFIX.get(self.venv.variant, "pappo")
         return "load_model/parameters/{}-{:02d}-{}-step-{:03d}000.npy".format(pre, self.num_algo, name,
@@ -316,6 +324,7 @@ class Algo_PPO:
 
     def save_reward_curves(self):
         """(:908-916) reward_cross / reward_wait / reward_choice / scenario_balance."""
+        self._flush_curves()
         os.makedirs("load_model/parameters", exist_ok=True)
         for name, v in (("reward_cross", np.array(self.ep_reward_cross)), ("reward_wait", np.array(self.ep_reward_wait)),
                         ("reward_choice", np.array(self.ep_reward_choice)),
@@ -358,6 +367,7 @@ class Algo_PPO:
     def save_checkpoint(self, path):
         """Everything needed to continue training bit-identically.  Under data parallelism
         every rank writes `path.rank<r>` (its env shard differs; nets/Adam are replicated)."""
+        self._flush_curves()  # the newest iteration's curve entries may still be in flight
         ck = {
             "nets": {f"{k}_{h}": getattr(self, f"{k}_net_{h}").state_dict() for h in ("cross", "wait", "choice")
                      for k in ("actor", "critic")},

@@ -142,15 +142,24 @@ class VecCrosswalk:
                 int(c.sin_model), int(c.flags), float(c.dt), [float(x) for x in c.car_b], [float(x) for x in c.ped_b],
                 [float(x) for x in c.cross_b], int(c.seed_base), int(c.env_id_offset)]
 
+    # Layout version of the exported device blob (mhppo_env_export): bump whenever the blob's
+    # layout changes, even at the same size.  2 = r03 layout (event counters before the MT blocks,
+    # the 4-block MT19937 ring, EI_MTB = active block + stale bits); 1 = r02 (2 MT blocks).
+    STATE_LAYOUT = 2
+
     def state_dict(self):
         """Whole device state (all env fields + every env's MT19937 stream), for exact resume."""
         L = _lib.lib()
         n = int(L.mhppo_env_state_bytes(self._h))
         blob = torch.empty(n, dtype=torch.uint8, device=self.device)
         _lib.check(L.mhppo_env_export(self._h, _lib.ptr(blob), _lib.stream_ptr(device=self.device)))
-        return {"cfg": self._cfg_key(), "blob": blob.cpu()}
+        return {"cfg": self._cfg_key(), "layout": self.STATE_LAYOUT, "blob": blob.cpu()}
 
     def load_state_dict(self, sd):
+        lay = int(sd.get("layout", 1))
+        if lay != self.STATE_LAYOUT:
+            raise ValueError(f"env checkpoint has state layout {lay}, this build reads layout {self.STATE_LAYOUT} "
+                             "(the blob layout changed between versions; it cannot be converted)")
         if list(sd["cfg"]) != self._cfg_key():
             raise ValueError("env checkpoint was made for another configuration")
         L = _lib.lib()

@@ -31,3 +31,30 @@ def test_reward_curve_paths_match_reference_format():
     ref = "load_model/parameters/pappo-scalable-coop-{num_algo:02d}-{name}-step-{epoch:03d}000.npy"
     for name in ("reward_cross", "reward_wait", "reward_choice", "scenario_balance"):
         assert a._curve_path(name) == ref.format(num_algo=111, epoch=1, name=name)
+
+
+def test_env_checkpoint_layout_version_is_checked():
+    import pytest
+    from mhppo.env import VecCrosswalk
+
+    class _E:
+        STATE_LAYOUT = VecCrosswalk.STATE_LAYOUT
+
+        def _cfg_key(self):
+            return [0]
+    for old in ({"cfg": [0], "blob": None}, {"cfg": [0], "layout": VecCrosswalk.STATE_LAYOUT - 1, "blob": None}):
+        with pytest.raises(ValueError, match="state layout"):
+            VecCrosswalk.load_state_dict(_E(), old)
+
+
+def test_curves_flush_pending_entries():
+    import torch
+    a = _algo(1, 0)
+    a.ep_reward_cross, a.ep_reward_wait, a.ep_reward_choice, a.ep_scenario_balance = [], [], [], []
+
+    class _Ev:
+        def synchronize(self):
+            pass
+    a._pending_curves = [(torch.tensor([2.0, 6.0, 3.0], dtype=torch.float64), _Ev(), 2.0, 3.0, 1.0)]
+    c, w, d, b = a.curves()
+    assert (c, w, d, b) == ([1.0], [2.0], [3.0], [[2, 3]]) and a._pending_curves == []

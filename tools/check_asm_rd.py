@@ -1,0 +1,136 @@
+"""Build-time ISA check of the split-precision train kernel's in-gap LDS reads (csrc/mlp_train.hip
+X3_MACC6_RD).
+
+Those inline-asm blocks issue six ds_read_b64_tr_b16 between their MFMAs and hand the
+destination registers to the compiler as if the data were ready; the next block waits with
+"s_waitcnt lgkmcnt(0)" before its MFMAs read them.  That is correct only if the register
+allocator leaves those VGPRs untouched until that wait: a v_mov copy, a spill or a
+rematerialisation in between would read (or clobber) registers whose LDS data is still in
+flight and silently corrupt the weight gradients.  This script checks the invariant on the
+code object actually built: for every ds_read_b64_tr_b16 issued right after an MFMA (the
+in-gap reads; the compiler's own reads are waited for by its own counters), no instruction
+may read or write any of its destination VGPRs before the next s_waitcnt lgkmcnt(0), and no
+branch or label may intervene.
+
+usage: python tools/check_asm_rd.py [libmhppo.so]   (exit 1 on a violation)"""
+import os
+import re
+import struct
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+KERNEL = "k_mlp_train_x3"
+
+
+def code_objects(path):
+    """The gfx950 code objects of every clang offload bundle embedded in a host binary."""
+    d = open(path, "rb").read()
+    i = 0
+    while True:
+        i = d.find(MAGIC, i)
+        if i < 0:
+            return
+        n = struct.unpack_from("<Q", d, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, ts = struct.unpack_from("<QQQ", d, p)
+            p += 24
+            triple = d[p:p + ts].decode()
+            p += ts
+            if "gfx950" in triple and size:
+                yield d[i + off:i + off + size]
+        i += len(MAGIC)
+
+
+def regs(tok):
+    """VGPR numbers named by one operand token (v7, v[4:5])."""
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"v(\d+)", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def parse(line):
+    """(mnemonic, [operand tokens]) of one objdump instruction line, or None."""
+    t = line.split("//")[0].strip()
+    if not t or t.endswith(":") or t.startswith("<"):
+        return None
+    op, _, rest = t.partition(" ")
+    return op, [o.strip() for o in rest.split(",") if o.strip()]
+
+
+def check_function(name, lines):
+    """Violations in one kernel's disassembly (list of strings)."""
+    bad, n_reads = [], 0
+    insts = [(ln, parse(ln)) for ln in lines]
+    for k, (ln, pi) in enumerate(insts):
+        if not pi or pi[0] != "ds_read_b64_tr_b16":
+            continue
+        prev = next((q for q in reversed(insts[:k]) if q[1]), None)
+        if prev is None or not prev[1][0].startswith("v_mfma"):
+            continue  # a compiler-placed read: its own counters cover it
+        n_reads += 1
+        pending = regs(pi[1][0])
+        for ln2, p2 in insts[k + 1:]:
+            if p2 is None:
+                if ln2.strip().endswith(":"):
+                    bad.append(f"{name}: label before the wait for {pi[1][0]} ({ln.strip()})")
+                    break
+                continue
+            op2, ops2 = p2
+            if op2 == "s_waitcnt" and "lgkmcnt(0)" in " ".join(ops2):
+                break
+            if op2.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
+                bad.append(f"{name}: branch before the wait for {pi[1][0]} ({ln.strip()})")
+                break
+            used = set().union(*[regs(o) for o in ops2]) if ops2 else set()
+            if op2 == "ds_read_b64_tr_b16":  # a later in-gap read: only its address may not overlap
+                used = set().union(*[regs(o) for o in ops2[1:]]) if len(ops2) > 1 else set()
+                if regs(ops2[0]) & pending:
+                    bad.append(f"{name}: {ln2.strip()} overwrites in-flight {pi[1][0]}")
+                    break
+            if used & pending:
+                bad.append(f"{name}: '{ln2.strip()}' touches in-flight {pi[1][0]} of '{ln.strip()}'")
+                break
+    return bad, n_reads
+
+
+def main(path):
+    total_reads, bad, nfun = 0, [], 0
+    for co in code_objects(path):
+        tmp = "/tmp/mhppo_check_asm_rd.co"
+        with open(tmp, "wb") as f:
+            f.write(co)
+        dis = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", tmp], capture_output=True, text=True,
+                             check=True).stdout
+        os.unlink(tmp)
+        if KERNEL not in dis:
+            continue
+        funcs = re.split(r"\n(?=[0-9a-f]+ <)", dis)
+        for fn in funcs:
+            head = fn.split("\n", 1)[0]
+            if KERNEL not in head:
+                continue
+            nfun += 1
+            b, n = check_function(head.strip(), fn.split("\n")[1:])
+            bad += b
+            total_reads += n
+    if nfun == 0:
+        print(f"check_asm_rd: no {KERNEL} kernel in {path}")
+        return 1
+    if total_reads == 0:
+        print("check_asm_rd: found no in-gap reads (did the asm blocks change?)")
+        return 1
+    for b in bad:
+        print("VIOLATION", b)
+    print(f"check_asm_rd: {nfun} kernels, {total_reads} in-gap ds_read_b64_tr_b16, {len(bad)} violations")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "mh-ppo_amd", "mhppo", "lib",
+                                                                        "libmhppo.so")))
