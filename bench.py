@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="one rank: init a one-rank RCCL group and run every data-parallel collective "
+                         "anyway (the multi-GPU call sequence on one GPU; identity sums)")
     ap.add_argument("--save-nets", default=None, help="rank 0 saves every net's flat weights here (tests)")
     ap.add_argument("--exact-f32", action="store_true",
                     help="continuous heads on the exact f32-MFMA train kernel (Algo_PPO(exact_f32=True))")
@@ -165,7 +168,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(a.dist_backend)
+    elif a.force_collectives:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29700 + os.getpid() % 200))
+        dist.init_process_group(a.dist_backend, rank=0, world_size=1,
+                                device_id=torch.device("cuda", local) if a.dist_backend == "nccl" else None)
     from mhppo import ppo
+    if a.force_collectives:
+        ppo.set_force_collectives(True)
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
@@ -235,8 +245,10 @@ def main():
         "config": {"workload": f"config {a.config}: {variant} nb_car={nc} nb_ped={npd} nb_lines={nl}, {N} envs/GPU x "
                                f"80 steps, full PPO iteration (rollout + returns + 10+10 epochs)",
                    "envs_per_gpu": N, "agents": agents, "T": T, "parallelism": f"dp{world}"},
-        "dist": {"world_size": world, "backend": (a.dist_backend if world > 1 else None),
-                 "env_ranges": [[r * N, (r + 1) * N] for r in range(world)]},
+        "dist": {"world_size": world, "backend": (a.dist_backend if dist.is_initialized() else None),
+                 "env_ranges": [[r * N, (r + 1) * N] for r in range(world)],
+                 "collectives": "forced (one rank)" if a.force_collectives and world == 1 else
+                 ("per epoch: advantage sums + gradient bucket" if world > 1 else "none (one rank)")},
         "roofline": {"bound": "mfma",
                      "kernel": ("k_mlp_train_x3 (fused continuous-head fwd/loss/bwd/wgrad, bf16x3-split MFMA, "
                                 "f32-equivalent FLOPs)" if split else
@@ -259,7 +271,7 @@ def main():
         np.save(a.save_nets, np.concatenate([net.flat().cpu().numpy() for net in algo.nets()]))
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

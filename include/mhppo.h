@@ -212,6 +212,9 @@ int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_roll
  * number of timed launches.  No reference counterpart. */
 int mhppo_kernel_timing_begin(int n);
 int mhppo_kernel_timing_end(double *ms_total, int *launches);
+/* As mhppo_kernel_timing_end, but writes each timed launch's milliseconds, in launch order, to
+ * ms_each[0 .. min(cap, launches)) (the per-step durations of a rollout: tools/env_steps.py). */
+int mhppo_kernel_timing_end_each(float *ms_each, int cap, int *launches);
 
 /* Status of the rollout launches queued on `stream` so far: synchronises the stream, reads
  * and clears bufs->status, and returns MHPPO_ENAN when a NaN policy output was drawn from

@@ -12,7 +12,7 @@
 // kernel, which differs from glibc in the last bit on ~20 % of inputs, and torch's Linear sums
 // in MKL's order, not the fmaf chain's.  Against the reference's own batch-1 forward the policy
 // outputs therefore agree to float32 rounding (tests/test_policy_torch_gpu.py: probabilities
-// within 8 ulps, actions within 1e-5, every Categorical draw identical on 4 096 rows).
+// within 1e-5 relative, actions within 1e-5, every Categorical draw identical on 4 096 rows).
 //   mhppo_tanhf  — sysdeps/ieee754/flt-32/s_tanhf.c (fdlibm): |x| >= 1: 1 - 2 / (expm1f(2|x|) + 2),
 //                  else -t / (t + 2) with t = expm1f(-2|x|); |x| >= 22: +-1; |x| < 2^-55: x (1 + x)
 //   mhppo_expm1f — sysdeps/ieee754/flt-32/s_expm1f.c (fdlibm): reduction x = k ln2 + r (ln2 split

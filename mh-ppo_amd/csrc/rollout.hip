@@ -750,7 +750,9 @@ __global__ void __launch_bounds__(bk::BTPB)
   __syncthreads();
   // the observation records of one step of the block's 64 segments are 64 x 13 consecutive
   // floats: lanes read them as one flat run (every load instruction on two 128-byte lines), all
-  // of a lane's loads issued before its first LDS store
+  // of a lane's loads issued before its first LDS store.  Only records of bucketed segments are
+  // loaded (exec-masked): the scalable env's non-existent slots (pos < 0) cost no fetch unless a
+  // bucketed neighbour shares their 128-byte line.
   {
     constexpr int NQ = SEGS * NF_C * STEPS / BTPB;
     static_assert(SEGS * NF_C * STEPS % BTPB == 0, "bucket scatter: block size");
@@ -759,9 +761,10 @@ __global__ void __launch_bounds__(bk::BTPB)
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
       const int i = tid + q * BTPB, tl = i / (SEGS * NF_C), k = i - tl * (SEGS * NF_C), sg = k / NF_C;
-      const bool in = sg < nseg && tl < nt;  // (in-range loads are unconditional: no branches)
+      const bool in = sg < nseg && tl < nt;
       at[q] = in && s_pos[sg] >= 0 ? sg * OBS_SEG + tl * NF_C + (k - sg * NF_C) : -1;
-      v[q] = obs[in ? ((int64_t)(t0 + tl) * NS + s0) * NF_C + k : 0];
+      v[q] = 0.0f;
+      if (at[q] >= 0) v[q] = obs[((int64_t)(t0 + tl) * NS + s0) * NF_C + k];
     }
 #pragma unroll
     for (int q = 0; q < NQ; q++)
@@ -1126,7 +1129,7 @@ int mhppo_kernel_timing_begin(int n) {
   return MHPPO_OK;
 }
 
-int mhppo_kernel_timing_end(double *ms_total, int *launches) {
+static int kernel_timing_collect(double *ms_total, float *ms_each, int cap, int *launches) {
   KernelTiming &k = g_ktime;
   const int used = k.used;
   k.on = false;  // off before anything can fail: later launches are untimed either way
@@ -1137,10 +1140,20 @@ int mhppo_kernel_timing_end(double *ms_total, int *launches) {
     float ms = 0.f;
     CHECK_HIP(hipEventElapsedTime(&ms, k.ev[2 * i], k.ev[2 * i + 1]));
     tot += ms;
+    if (ms_each && i < cap) ms_each[i] = ms;
   }
   if (ms_total) *ms_total = tot;
   if (launches) *launches = used;
   return MHPPO_OK;
+}
+
+int mhppo_kernel_timing_end(double *ms_total, int *launches) {
+  return kernel_timing_collect(ms_total, nullptr, 0, launches);
+}
+
+int mhppo_kernel_timing_end_each(float *ms_each, int cap, int *launches) {
+  if (cap < 0 || (cap > 0 && !ms_each)) return set_error(MHPPO_EINVAL, "kernel timing: bad output buffer");
+  return kernel_timing_collect(nullptr, ms_each, cap, launches);
 }
 
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {

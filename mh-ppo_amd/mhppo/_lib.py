@@ -73,6 +73,7 @@ _SIGS = {
     "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
     "mhppo_kernel_timing_begin": (I32, [I32]),
     "mhppo_kernel_timing_end": (I32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I32)]),
+    "mhppo_kernel_timing_end_each": (I32, [P, I32, ctypes.POINTER(I32)]),
     "mhppo_eval_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), I32,
                               ctypes.POINTER(EvalBufs), P]),
     "mhppo_rollout_check": (I32, [ctypes.POINTER(RolloutBufs), P]),

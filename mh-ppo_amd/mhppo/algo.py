@@ -7,6 +7,7 @@ environment is a VecCrosswalk of N envs: one `train` iteration plays one
 80-step episode in every env (the reference plays 26 episodes of one env for
 batch_size=2048), then runs the same 10 + 10 full-batch epochs.
 """
+import contextlib
 import os
 
 import numpy as np
@@ -202,7 +203,7 @@ class Algo_PPO:
         r = self.rollout
         dev = self.venv.device
         c, w, d = r.cross, r.wait, r.choice
-        with torch.cuda.device(dev):
+        with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
             counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
             if ppo._dp():  # global row counts: one all-reduce and one host sync
                 loc = torch.cat([torch.tensor([c["ret"].numel(), w["ret"].numel(), d["ret"].numel()],
@@ -271,13 +272,16 @@ class Algo_PPO:
             dev = self.venv.device
             sums = torch.stack([rc.double().sum(), rw.double().sum(), rd.double().sum()]).to(dev)
             ppo._allreduce_(sums)
-            # the reward curves take the sums without a host sync here: an asynchronous copy to
-            # pinned memory, appended once it has landed (next iteration, or the end of train)
-            host = torch.empty(3, dtype=torch.float64, pin_memory=True)
-            host.copy_(sums, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            self._pending_curves.append((host, ev, m_c, m_w, m_d))
+            if dev.type == "cuda":
+                # the reward curves take the sums without a host sync here: an asynchronous copy to
+                # pinned memory, appended once it has landed (next iteration, or the end of train)
+                host = torch.empty(3, dtype=torch.float64, pin_memory=True)
+                host.copy_(sums, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                self._pending_curves.append((host, ev, m_c, m_w, m_d))
+            else:  # (CPU test doubles of the rollout: tests/test_dp_gloo.py)
+                self._pending_curves.append((sums.clone(), None, m_c, m_w, m_d))
             if self.verbose:
                 self._flush_curves()
             if self.verbose and _rank() == 0:
@@ -302,7 +306,8 @@ class Algo_PPO:
         the iterations whose reward sums have been read back."""
         n = len(self._pending_curves) - (1 if keep_last else 0)
         for host, ev, m_c, m_w, m_d in self._pending_curves[:n]:
-            ev.synchronize()
+            if ev is not None:
+                ev.synchronize()
             s = host.tolist()
             if m_c > 0:
                 self.ep_reward_cross.append(s[0] / m_c)

@@ -32,8 +32,22 @@ import torch.distributed as dist
 from . import _lib
 
 
+_FORCE_COLLECTIVES = False
+
+
+def set_force_collectives(flag=True):
+    """Run the data-parallel collectives even in a one-rank process group (they are skipped
+    when world_size == 1): a one-GPU RCCL rehearsal of the exact multi-GPU call sequence
+    (bench.py --force-collectives, tests/dp_worker.py --nccl-world1).  Needs an initialised
+    process group; a one-rank SUM is the identity, so results equal the plain run's."""
+    global _FORCE_COLLECTIVES
+    _FORCE_COLLECTIVES = bool(flag)
+
+
 def _dp():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return _FORCE_COLLECTIVES or dist.get_world_size() > 1
 
 
 def _allreduce_(t):

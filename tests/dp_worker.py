@@ -27,7 +27,7 @@ if a.nccl_world1:
     os.environ.setdefault("MASTER_PORT", str(29900 + os.getpid() % 90))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from mhppo import ppo  # noqa: E402
-    ppo._dp = lambda: True  # the update's collectives run (one rank: identity sums)
+    ppo.set_force_collectives(True)  # the update's collectives run (one rank: identity sums)
 elif world > 1:
     dist.init_process_group("gloo")  # rehearsal: the ranks share the box's one GPU
 from mhppo.algo import Algo_PPO  # noqa: E402

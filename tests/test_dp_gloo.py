@@ -238,3 +238,115 @@ def test_dp2_joint_epoch_skipped_middle_head():
         np.testing.assert_allclose(a, b_, rtol=0, atol=2e-6)
     for g in dp2[-2:]:  # the skipped head's gradient slices: untouched by any collective
         assert np.all(g == 1.0)
+
+
+# ------------------------------------------------------------------ whole Algo_PPO.train, world 4
+class _Cfg:
+    car_b = [-4.0, 0.0, 2.0, 0.0]
+
+
+class _VenvDouble:
+    """The attributes Algo_PPO reads from a VecCrosswalk (CPU; no env handle)."""
+
+    def __init__(self, n_envs, env_id_offset):
+        self.n_envs, self.env_id_offset = n_envs, env_id_offset
+        self.max_episode, self.n_slots, self.dt, self.variant = 8, 2, 0.5, "coop"
+        self.cfg, self.device = _Cfg(), torch.device("cpu")
+
+
+def _rollout_double_class(n_total):
+    """Env_rollout stand-in: one 'episode' per env, each (env, slot) segment bucketed by its GLOBAL
+    env id, so rank r of W owns exactly the global segments [r n, (r + 1) n) of one process.
+    Quarter 1 of the envs is all cross, quarter 2 all wait: with 4 ranks, rank 1 has no wait
+    rows and rank 2 no cross rows (each still joins every collective)."""
+
+    class RolloutDouble:
+        def __init__(self, env, nb_cars, max_steps, dt):
+            self.env, self.T = env, max_steps
+            self.seed, self.iteration, self.fix_bucket = 0, 0, False
+            self.cross = self.wait = self.choice = None
+
+        def reset(self):
+            pass
+
+        def iterations_rand(self, *a, **k):
+            T, S = self.T, self.env.n_slots
+            seg = {"cross": [], "wait": []}
+            ch = []
+            for g in range(self.env.env_id_offset, self.env.env_id_offset + self.env.n_envs):
+                q = 4 * g // n_total
+                for s in range(S):
+                    rng = np.random.default_rng(1000 * self.iteration + 10 * g + s)
+                    b = "cross" if q == 1 else ("wait" if q == 2 else ("cross" if rng.uniform() < 0.5 else "wait"))
+                    seg[b].append((rng.normal(0, 3, (T, 13)).astype(np.float32), rng.normal(-1, 1, T).astype(np.float32),
+                                   rng.normal(-0.6, 0.3, T).astype(np.float32), rng.normal(-20, 8, T).astype(np.float32),
+                                   rng.normal(-1, 0.5, T)))
+                    ch.append((rng.normal(0, 2, 20).astype(np.float32), int(rng.uniform() < 0.4),
+                               np.float32(rng.normal(-0.7, 0.2)), np.float32(rng.normal(-3, 1))))
+            self.iteration += 1
+            for b in ("cross", "wait"):
+                L = seg[b]
+                cat = (lambda i, shape, dt: torch.from_numpy(np.concatenate([x[i] for x in L])) if L
+                       else torch.zeros(shape, dtype=dt))
+                d = dict(obs=cat(0, (0, 13), torch.float32), act=cat(1, (0,), torch.float32),
+                         logp=cat(2, (0,), torch.float32), ret=cat(3, (0,), torch.float32),
+                         rew=cat(4, (0,), torch.float64), n_seg=len(L))
+                setattr(self, b, d)
+            self.choice = dict(obs=torch.from_numpy(np.stack([c[0] for c in ch])),
+                               act=torch.tensor([c[1] for c in ch], dtype=torch.int32),
+                               logp=torch.tensor([c[2] for c in ch]), ret=torch.tensor([c[3] for c in ch]),
+                               n_seg=len(ch))
+
+        def immediate_rewards(self):
+            return self.cross["rew"].float(), self.wait["rew"].float(), self.choice["ret"]
+
+    return RolloutDouble
+
+
+def _run_algo(rank, world, port, n_total, out_q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
+    from mhppo import algo as algo_mod
+    from mhppo import ppo
+    from mhppo.models import Model_PPO
+    _install_cpu_doubles(ppo)
+    algo_mod.Env_rollout = _rollout_double_class(n_total)
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = n_total // world
+    torch.manual_seed(0)
+    a = algo_mod.Algo_PPO(Model_PPO, _VenvDouble(n, rank * n), verbose=False, save_curves=False, num_states_d=20)
+    a.train(2)
+    if rank == 0:
+        out_q.put([p.detach().numpy().copy() for net in a.nets() for p in net.parameters()] +
+                  [np.array(x, dtype=np.float64) for x in a.curves()])
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _spawn_algo(world, n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31700 + os.getpid() % 1000 + world
+    procs = [ctx.Process(target=_run_algo, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_dp4_algo_train_uneven_shards():
+    """Two whole Algo_PPO.train iterations (update: global row and action counts, the joint
+    epochs' advantage-sum and gradient-bucket all-reduces, replicated Adam; the reward-curve sum
+    all-reduce) over 4 gloo ranks equal one process on all envs.  Rank 1 holds no wait rows and
+    rank 2 no cross rows."""
+    n_total = 64
+    single = _spawn_algo(1, n_total)
+    dp4 = _spawn_algo(4, n_total)
+    assert len(single) == len(dp4)
+    for a, b in zip(single, dp4):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=2e-6)
+    assert len(single[-4]) == 2  # two reward-curve entries per head

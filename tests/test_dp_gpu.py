@@ -68,3 +68,25 @@ def test_rccl_collectives_one_rank(tmp_path):
     a, b = np.load(one), np.load(rc)
     assert np.isfinite(a).all()
     np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)
+
+
+def test_bench_force_collectives_rccl(tmp_path):
+    """`bench.py --force-collectives` on one GPU: a one-rank RCCL group with every data-parallel
+    collective of the product's update issued (ppo.set_force_collectives, no monkey-patching)
+    trains the same nets as the plain run."""
+    import json
+    one, rc = str(tmp_path / "one.npy"), str(tmp_path / "rc.npy")
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    common = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--envs", "1024", "--steps", "1",
+              "--warmup", "0", "--no-cpu-baseline"]
+    subprocess.run(common + ["--save-nets", one], check=True, timeout=300, env=env, cwd=tmp_path,
+                   capture_output=True, text=True)
+    out = subprocess.run(common + ["--save-nets", rc, "--force-collectives"], check=True, timeout=300, env=env,
+                         cwd=tmp_path, capture_output=True, text=True).stdout
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    assert line["dist"]["backend"] == "nccl" and line["dist"]["collectives"].startswith("forced")
+    a, b = np.load(one), np.load(rc)
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(b, a, rtol=0, atol=1e-6)

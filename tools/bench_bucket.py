@@ -1,7 +1,7 @@
 """Time mhppo_bucket_scatter at the bench's shape (config 3: NS = 65 536 envs x 4 slots
 segments, T = 80 steps, ~half the segments in each bucket) with HIP events on the launch
 stream.  MHPPO_LIB selects the library build (A/B).  Prints ms per launch and the HBM rate
-over the algorithmic bytes (72 B per record read, 72 B per bucketed record written)."""
+over the algorithmic bytes (72 B read + 72 B written per bucketed record)."""
 import os
 import sys
 
@@ -17,7 +17,10 @@ obs = torch.randn(T, NS, NF, device=dev, generator=g)
 act, logp, ret = (torch.randn(T, NS, device=dev, generator=g) for _ in range(3))
 rew = torch.randn(T, NS, device=dev, dtype=torch.float64, generator=g)
 u = torch.rand(NS, device=dev, generator=g)
-segs = [torch.nonzero(u < 0.5).squeeze(1), torch.nonzero(u >= 0.5).squeeze(1)]
+# EXIST < 1: that fraction of segments exists (the scalable env's ragged slots); the rest are in
+# neither bucket (pos = -1) and must not be fetched
+ex = torch.rand(NS, device=dev, generator=g) < float(os.environ.get("EXIST", "1"))
+segs = [torch.nonzero((u < 0.5) & ex).squeeze(1), torch.nonzero((u >= 0.5) & ex).squeeze(1)]
 pos = torch.full((NS,), -1, dtype=torch.int64, device=dev)
 bucket = torch.zeros(NS, dtype=torch.int8, device=dev)
 dst, keep = (_lib.BucketDst * 2)(), []
@@ -49,6 +52,6 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / K
 nrec = T * NS
-byts = 72 * nrec + 72 * T * sum(s.numel() for s in segs)
+byts = 144 * T * sum(s.numel() for s in segs)  # bucketed records: read + written
 print(f"{os.environ.get('TAG', 'lib')}: bucket_scatter {ms * 1e3:.1f} us  {byts / ms / 1e6:.0f} GB/s "
       f"({byts / 1e9:.3f} GB algorithmic)")
