@@ -306,6 +306,20 @@ int mhppo_mlp_train(int kind, int n_in, const float *packed, const float *X, int
                     const double *counts, double m_global, float out_mean, float out_std, float *grad,
                     double *sums, void *stream);
 
+/* One epoch step of a continuous head run as a pipeline (Algo_PPO.train_model_c :778-815, epochs
+ * e and e + 1 overlapped): the ACTOR pass of epoch e (kind 1 of mhppo_mlp_train: advantage
+ * A = ret - value normalised with `stats`, the critic pass e's (sum A, sum A^2) over m_global
+ * rows) and the CRITIC pass of epoch e + 1 (kind 0, with the critic's weights after its Adam step
+ * e) in ONE launch over the same rows: one input load per tile for both nets.  `value` holds V_e
+ * on entry and V_{e+1} on return (each row is read before it is overwritten).  grad_* / sums_*
+ * as mhppo_mlp_train's (sums_actor += (sum surrogate, 0, 0), sums_critic += (sum (V-G)^2,
+ * sum A, sum A^2) of epoch e + 1).  bf16x3 split-precision kernel only (13 inputs, 1 output). */
+int mhppo_mlp_train_pair(const float *packed_actor, const float *packed_critic, const float *X, int64_t M,
+                         const float *ret, float *value, const float *act, const float *logp_old,
+                         const double *stats, double m_global, float out_mean, float out_std,
+                         float *grad_actor, double *sums_actor, float *grad_critic, double *sums_critic,
+                         void *stream);
+
 /* Critic MSE (:808-809): loss += sum (V-G)^2, dV = 2 (V-G) * inv_m. */
 int mhppo_mse_fwd_bwd(const float *value, const float *ret, int64_t M, double inv_m, float *dv,
                       double *loss, void *stream);

@@ -761,6 +761,8 @@ constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * LY::IN_SZ * 4, WAV
 constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int LDS_BYTES_PAIR = 2 * O_WAVE + WAVES * WAVE_B;  // two nets' weights (k_mlp_train_x3_pair)
+static_assert(LDS_BYTES_PAIR <= 160 * 1024, "LDS budget (pair)");
 static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
 
 #ifdef MHPPO_X3_PHASE
@@ -996,136 +998,149 @@ __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 // 256 registers (no hoisted fragments, h1 recomputed: 12 % slower), two tiles per wave in lock
 // step (spills), a software-pipelined loop (backward of tile i beside the forward of tile i+1:
 // 10 % slower).
-template <int KIND>
-__global__ void __launch_bounds__(64 * x3::WAVES)
-    k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
-                   float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
-                   const double *__restrict__ stats, double m_global, float out_mean, float out_std,
-                   float *__restrict__ gpart, double *__restrict__ dpart) {
-  using namespace x3;
-  extern __shared__ float lds[];
-  char *L8 = reinterpret_cast<char *>(lds);
-  const int tid = threadIdx.x, l = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+namespace x3 {
+constexpr int G_W1 = 0, G_B1 = 32 * NIN, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
+              G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
+constexpr int NET_B = O_WAVE;  // LDS bytes of one net's staged weights (bf16 images + f32 params)
+
+// Stage one net's weights at Lw: bf16 images (three parts), b1 as input column 13 of W1.  Every
+// global load is issued before the first LDS store (one memory round trip per launch; a strided
+// load -> split -> store loop per array costs one dependent trip per iteration).
+__device__ __forceinline__ void stage_net(const float *__restrict__ W, char *Lw, int tid) {
   constexpr int nin = NIN;
-  constexpr int G_W1 = 0, G_B1 = 32 * nin, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
-                G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
-  // ---- stage the weights: bf16 images (three parts), b1 as input column 13 of W1.  Every
-  // global load is issued before the first LDS store (one memory round trip per launch; a
-  // strided load -> split -> store loop per array costs one dependent trip per iteration).
-  float *F = reinterpret_cast<float *>(L8 + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
-  {
-    constexpr int NT = 64 * WAVES, N1 = (32 * 16 + NT - 1) / NT, N2 = 2048 / NT, NFQ = (NF + NT - 1) / NT;
-    static_assert(2048 % NT == 0, "staging: block size");
-    float v1[N1], v2[N2], v3[N2], vf[NFQ];
+  float *F = reinterpret_cast<float *>(Lw + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
+  constexpr int NT = 64 * WAVES, N1 = (32 * 16 + NT - 1) / NT, N2 = 2048 / NT, NFQ = (NF + NT - 1) / NT;
+  static_assert(2048 % NT == 0, "staging: block size");
+  float v1[N1], v2[N2], v3[N2], vf[NFQ];
 #pragma unroll
-    for (int q = 0; q < N1; q++) {
-      const int i = tid + q * NT, r = i >> 4, c = i & 15;
-      v1[q] = i >= 32 * 16 ? 0.0f : (c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f));
-    }
-#pragma unroll
-    for (int q = 0; q < N2; q++) {
-      v2[q] = W[G_W2 + tid + q * NT];
-      v3[q] = W[G_W3 + tid + q * NT];
-    }
-#pragma unroll
-    for (int q = 0; q < NFQ; q++) {
-      const int i = tid + q * NT;
-      vf[q] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
-    }
-#pragma unroll
-    for (int q = 0; q < N1; q++) {
-      const int i = tid + q * NT;
-      if (i < 32 * 16) stage_w(L8 + O_W1, W1_PART, W1_ROWB, i >> 4, i & 15, v1[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < N2; q++) {
-      const int i = tid + q * NT;
-      stage_w(L8 + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, v2[q]);
-      stage_w(L8 + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, v3[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < NFQ; q++) {
-      const int i = tid + q * NT;
-      if (i < NF) F[i] = vf[q];
-    }
+  for (int q = 0; q < N1; q++) {
+    const int i = tid + q * NT, r = i >> 4, c = i & 15;
+    v1[q] = i >= 32 * 16 ? 0.0f : (c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f));
   }
-  __syncthreads();
-  char *wb = L8 + O_WAVE + w * WAVE_B;  // this wave's image / f32 transpose slot
-  float *T = reinterpret_cast<float *>(wb);
-  float *inb = reinterpret_cast<float *>(wb + O_IN);
-  const int j = l & 31, kh = l >> 5;
-  const int G = l >> 4, q4 = (l >> 2) & 3, p4 = l & 3;
-  // lane address bases: every fragment access below is one of these plus a constant
-  const char *w1row = L8 + O_W1 + j * W1_ROWB + 16 * kh;
-  const char *w2row = L8 + O_W2 + j * W2_ROWB + 8 * kh;
-  const char *w3row = L8 + O_W3 + j * W3_ROWB + 8 * kh;
-  const char *w2tr = L8 + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *w3tr = L8 + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
-  char *imw = wb + j * IM_ROWB + 8 * kh;
-  // image reads: rows 8 (G >> 1) + 4u + q, chunk 4 (G & 1) + p
-  const char *imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
-  const char *imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
-  const float b40 = uniform_f(F[128]);
-  // Loop-invariant weight fragments read from LDS once: the backward W^T ones, and for the
-  // critic pass the forward ones too (the actor pass's loss needs those registers)
-  constexpr bool HF = KIND == K_CRITIC;
+#pragma unroll
+  for (int q = 0; q < N2; q++) {
+    v2[q] = W[G_W2 + tid + q * NT];
+    v3[q] = W[G_W3 + tid + q * NT];
+  }
+#pragma unroll
+  for (int q = 0; q < NFQ; q++) {
+    const int i = tid + q * NT;
+    vf[q] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
+  }
+#pragma unroll
+  for (int q = 0; q < N1; q++) {
+    const int i = tid + q * NT;
+    if (i < 32 * 16) stage_w(Lw + O_W1, W1_PART, W1_ROWB, i >> 4, i & 15, v1[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < N2; q++) {
+    const int i = tid + q * NT;
+    stage_w(Lw + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, v2[q]);
+    stage_w(Lw + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, v3[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < NFQ; q++) {
+    const int i = tid + q * NT;
+    if (i < NF) F[i] = vf[q];
+  }
+}
+
+// The per-wave lane geometry of the wave's LDS slot (images, f32 transpose image, input slots)
+struct WaveSlot {
+  char *wb;          // this wave's image / f32 transpose slot
+  float *T;          // f32 transpose image (shares the slot)
+  float *inb;        // input slots (double buffered)
+  char *imw;         // image write base
+  const char *imr;   // image transposed-read base (32x32x16 operands)
+  const char *imr16; // image transposed-read base (16x16x32 operands)
+  int l, j, kh, G;
+  __device__ __forceinline__ WaveSlot(char *L8, int w, int l_) : l(l_), j(l_ & 31), kh(l_ >> 5), G(l_ >> 4) {
+    const int q4 = (l >> 2) & 3, p4 = l & 3;
+    wb = L8 + w * WAVE_B;
+    T = reinterpret_cast<float *>(wb);
+    inb = reinterpret_cast<float *>(wb + O_IN);
+    imw = wb + j * IM_ROWB + 8 * kh;
+    // image reads: rows 8 (G >> 1) + 4u + q, chunk 4 (G & 1) + p
+    imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
+    imr16 = wb + (8 * G + q4) * IM_ROWB + 8 * p4;  // 16x16x32 A: rows 8G + 4u + q, chunk 4t + p
+  }
+};
+
+// One net's pass over 32-row tiles (forward, loss gradient, backward, weight gradients), with its
+// per-wave state: lane bases into its staged weights, the loop-invariant weight fragments, the
+// weight-gradient accumulators and the bias / loss sums.  HF: the forward weight fragments are
+// held in registers too (one critic pass alone; the actor pass's loss, and a second net in the
+// same wave, need those registers) — and then dW2 cannot carry its image reads in its MFMA gaps.
+// HB: the backward (W^T) fragments are held in registers (not with two nets in one wave).
+template <int KIND, bool HF, bool HB = true>
+struct Pass {
+  const char *w1row, *w2row, *w3row, *w2tr, *w3tr;
+  const float *F;
+  float b40;
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
-  if constexpr (HF) {
-    for (int t = 0; t < 2; t++)
-      for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
-    for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
-  }
-  for (int t = 0; t < 2; t++)
-    for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
-  for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
-  auto fw2 = [&](int t, int s) -> F3 {
-    if constexpr (HF) return wf2[t][s];
-    else return w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
-  };
-  auto fw3 = [&](int s) -> F3 {
-    if constexpr (HF) return wf3[s];
-    else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
-  };
-  auto bw3 = [&](int t, int s) -> F3 { return wb3[t][s]; };
-  auto bw2 = [&](int s) -> F3 { return wb2[s]; };
-  f32x16 gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
-  f32x4 gW1t[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  // bias-gradient row sums (lane j, half kh: the half-tile sums of feature j)
-  float gsum[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // gB2a gB2b gB3 gW4 gB4
-  auto radd = [&](int k, float v) { gsum[k] += v; };
+  f32x16 gW2a, gW2b, gW3a, gW3b;
+  f32x4 gW1t[2];
+  float gsum[5];  // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4 gB4
   // float64 loss / advantage sums in registers (lanes kh == 0), folded once after the loop: an
   // LDS read-modify-write per tile put its latency on the loss section's serial chain (-1 %)
-  double dsum0 = 0.0, dsum1 = 0.0, dsum2 = 0.0;
-  float meanf = 0.f, stdf = 1.f;
-  if (KIND != K_CRITIC) {
-    double mean = stats[0] / m_global;
-    double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
-    meanf = uniform_f((float)mean);
-    stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
-  }
-  const double inv_m = uniform_d(1.0 / m_global);
-  const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
-  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+  double dsum0, dsum1, dsum2;
 
-  int cb = 0;
-  MHPPO_MARK(0);
-  if (gw < nfull) prefetch_tile<KIND, LY>(inb, X, ret, V, act, lp_old, gw * 32, l);
-  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
-    const int64_t row0 = tile * 32;
-    const int nrows = (int)min((int64_t)32, M - row0);
-    float *slot = inb + cb * LY::IN_SZ;
-    const int64_t nxt = tile + nw;
-    if (nxt < nfull) {
-      prefetch_tile<KIND, LY>(inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
-      wait_vmcnt<prefetch_ops<KIND>()>();
-    } else if (tile < nfull) {
-      wait_vmcnt<0>();
-    } else {
-      load_tile_sync<KIND, LY>(slot, X, nin, ret, V, act, lp_old, row0, nrows, l);
+  __device__ __forceinline__ void init(const char *Lw, const WaveSlot &ws) {
+    const int j = ws.j, kh = ws.kh, G = ws.G, q4 = (ws.l >> 2) & 3, p4 = ws.l & 3;
+    // lane address bases: every fragment access is one of these plus a constant
+    w1row = Lw + O_W1 + j * W1_ROWB + 16 * kh;
+    w2row = Lw + O_W2 + j * W2_ROWB + 8 * kh;
+    w3row = Lw + O_W3 + j * W3_ROWB + 8 * kh;
+    w2tr = Lw + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
+    w3tr = Lw + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
+    F = reinterpret_cast<const float *>(Lw + O_F);
+    b40 = uniform_f(F[128]);
+    // loop-invariant weight fragments read from LDS once
+    if constexpr (HF) {
+      for (int t = 0; t < 2; t++)
+        for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
+      for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
     }
-    wave_sync();  // the tile's inputs have landed
-    MHPPO_MARK(1);  // timing builds: the tile-input wait
+    if constexpr (HB) {
+      for (int t = 0; t < 2; t++)
+        for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
+      for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
+    }
+    gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
+    gW1t[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gW1t[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 5; k++) gsum[k] = 0.f;
+    dsum0 = dsum1 = dsum2 = 0.0;
+  }
+  __device__ __forceinline__ F3 fw2(int t, int s) const {
+    if constexpr (HF) return wf2[t][s];
+    else return w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
+  }
+  __device__ __forceinline__ F3 fw3(int s) const {
+    if constexpr (HF) return wf3[s];
+    else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
+  }
+  __device__ __forceinline__ F3 bw3(int t, int s) const {
+    if constexpr (HB) return wb3[t][s];
+    else return w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
+  }
+  __device__ __forceinline__ F3 bw2(int s) const {
+    if constexpr (HB) return wb2[s];
+    else return w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
+  }
+
+  // One 32-row tile whose inputs sit in `slot` (X [32][13] | ret V | act logp_old).  The critic
+  // writes V (rows row0 .. row0 + nrows) to Vout; the actor normalises A = ret - V with
+  // (meanf, stdf).
+  __device__ __forceinline__ void tile(const WaveSlot &ws, const float *slot, int64_t row0, int nrows,
+                                       float *__restrict__ Vout, float meanf, float stdf, double inv_m,
+                                       float out_mean, float out_std) {
+    constexpr int nin = NIN;
+    const int l = ws.l, j = ws.j, kh = ws.kh, G = ws.G;
+    float *T = ws.T;
+    char *imw = ws.imw;
+    const char *imr = ws.imr, *imr16 = ws.imr16;
+    auto radd = [&](int k, float v) { gsum[k] += v; };
     const float *Xs = slot + LY::IN_X;
     // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
     auto layer1 = [&]() {
@@ -1178,7 +1193,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
       const float rt = slot[LY::IN_S0 + j];
       if constexpr (KIND == K_CRITIC) {
         const float v = y0;
-        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
+        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 128), 4 * j, 0, 0);
         const float a = rt - v;
         const float d = v - rt;
         if (kh == 0) {
@@ -1265,7 +1280,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     MHPPO_MARK(7);
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
     f32x16 d1 = zero16();
-    if constexpr (KIND != K_CRITIC) {
+    if constexpr (!HF) {
       const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
       d1 = mfma6(bw2(0), f0, d1);
       d1 = mfma6(bw2(1), f1, d1);
@@ -1292,7 +1307,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
         macc6_w(db1, bh1, gW2b);
       }
       lds_order();
-    } else {  // (the critic pass holds its forward weight fragments: no registers for the reads ahead)
+    } else {  // (the forward weight fragments are held: no registers for the reads ahead)
       const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
       d1 = mfma6(bw2(0), f0, d1);
       d1 = mfma6(bw2(1), f1, d1);
@@ -1341,56 +1356,167 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     x3_phase();
     MHPPO_MARK(9);
   }
-  // ---- write this wave's partial gradient (packed torch layout)
-  MHPPO_MARK_FLUSH();
-  macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
-  float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
-  float *gp = gpart + (size_t)gw * NWP;
+
+  // this wave's partial gradient (packed torch layout) and float64 sums
+  __device__ __forceinline__ void finish(const WaveSlot &ws, float *__restrict__ gp, double *__restrict__ dp) {
+    constexpr int nin = NIN;
+    const int l = ws.l, j = ws.j, kh = ws.kh, G = ws.G;
+    macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
+    float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int f = feat(r, l);
-    gp[G_W2 + f * 32 + j] = gW2a[r];
-    gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
-    gp[G_W3 + f * 64 + j] = gW3a[r];
-    gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
-  }
+    for (int r = 0; r < 16; r++) {
+      const int f = feat(r, l);
+      gp[G_W2 + f * 32 + j] = gW2a[r];
+      gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
+      gp[G_W3 + f * 64 + j] = gW3a[r];
+      gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
+    }
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < 2; t++) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int f = 16 * t + 4 * G + r, n = l & 15;
-      if (n < nin) gp[G_W1 + f * nin + n] = gW1t[t][r];
-      if (n == nin) gp[G_B1 + f] = gW1t[t][r];
+      for (int r = 0; r < 4; r++) {
+        const int f = 16 * t + 4 * G + r, n = l & 15;
+        if (n < nin) gp[G_W1 + f * nin + n] = gW1t[t][r];
+        if (n == nin) gp[G_B1 + f] = gW1t[t][r];
+      }
+    }
+    // halves of the row sums: lanes j and j + 32 hold rows 0-15 / 16-31 of feature j
+    gB2a += __shfl_xor(gB2a, 32);
+    gB2b += __shfl_xor(gB2b, 32);
+    gB3 += __shfl_xor(gB3, 32);
+    gW4 += __shfl_xor(gW4, 32);
+    if (kh == 0) {
+      gp[G_B2 + j] = gB2a;
+      gp[G_B2 + 32 + j] = gB2b;
+      gp[G_B3 + j] = gB3;
+      gp[G_W4 + j] = gW4;
+    }
+    float b4s0 = gB4;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (kh == 0) s0 = dsum0, s1 = dsum1, s2 = dsum2;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 += __shfl_xor(s1, o);
+      s2 += __shfl_xor(s2, o);
+    }
+    if (l == 0) {
+      gp[G_B4] = b4s0;
+      dp[0] = s0;
+      dp[1] = s1;
+      dp[2] = s2;
     }
   }
-  // halves of the row sums: lanes j and j + 32 hold rows 0-15 / 16-31 of feature j
-  gB2a += __shfl_xor(gB2a, 32);
-  gB2b += __shfl_xor(gB2b, 32);
-  gB3 += __shfl_xor(gB3, 32);
-  gW4 += __shfl_xor(gW4, 32);
-  if (kh == 0) {
-    gp[G_B2 + j] = gB2a;
-    gp[G_B2 + 32 + j] = gB2b;
-    gp[G_B3 + j] = gB3;
-    gp[G_W4 + j] = gW4;
+};
+
+// the normalisation of the actor's advantage from the critic pass's global sums
+__device__ __forceinline__ void adv_norm(const double *stats, double m_global, float &meanf, float &stdf) {
+  double mean = stats[0] / m_global;
+  double var = (stats[1] - stats[0] * mean) / (m_global - 1.0);
+  meanf = uniform_f((float)mean);
+  stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
+}
+
+// Inputs of this wave's tiles: LDS-DMA one tile ahead into the double-buffered slot; the ragged
+// last tile loads synchronously.  body(slot, row0, nrows) runs each tile.
+template <int KIND, class Body>
+__device__ __forceinline__ void tile_loop(const WaveSlot &ws, int64_t gw, int64_t nw, int64_t M, const float *X,
+                                          const float *ret, const float *V, const float *act, const float *lp_old,
+                                          Body &&body) {
+  const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
+  int cb = 0;
+  MHPPO_MARK(0);
+  if (gw < nfull) prefetch_tile<KIND, LY>(ws.inb, X, ret, V, act, lp_old, gw * 32, ws.l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
+    const int64_t row0 = tile * 32;
+    const int nrows = (int)min((int64_t)32, M - row0);
+    float *slot = ws.inb + cb * LY::IN_SZ;
+    const int64_t nxt = tile + nw;
+    if (nxt < nfull) {
+      prefetch_tile<KIND, LY>(ws.inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, ws.l);
+      wait_vmcnt<prefetch_ops<KIND>()>();
+    } else if (tile < nfull) {
+      wait_vmcnt<0>();
+    } else {
+      load_tile_sync<KIND, LY>(slot, X, NIN, ret, V, act, lp_old, row0, nrows, ws.l);
+    }
+    wave_sync();  // the tile's inputs have landed
+    MHPPO_MARK(1);  // timing builds: the tile-input wait
+    body(slot, row0, nrows);
   }
-  float b4s0 = gB4;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  if (kh == 0) s0 = dsum0, s1 = dsum1, s2 = dsum2;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s0 += __shfl_xor(s0, o);
-    s1 += __shfl_xor(s1, o);
-    s2 += __shfl_xor(s2, o);
-  }
-  if (l == 0) {
-    gp[G_B4] = b4s0;
-    dpart[gw * 3 + 0] = s0;
-    dpart[gw * 3 + 1] = s1;
-    dpart[gw * 3 + 2] = s2;
-  }
+  MHPPO_MARK_FLUSH();
+}
+}  // namespace x3
+
+template <int KIND>
+__global__ void __launch_bounds__(64 * x3::WAVES)
+    k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
+                   float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
+                   const double *__restrict__ stats, double m_global, float out_mean, float out_std,
+                   float *__restrict__ gpart, double *__restrict__ dpart) {
+  using namespace x3;
+  extern __shared__ float lds[];
+  char *L8 = reinterpret_cast<char *>(lds);
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  stage_net(W, L8, tid);
+  __syncthreads();
+  const WaveSlot ws(L8 + NET_B, w, l);
+  // the critic pass alone holds its forward weight fragments in registers
+  Pass<KIND, KIND == K_CRITIC> p;
+  p.init(L8, ws);
+  float meanf = 0.f, stdf = 1.f;
+  if (KIND != K_CRITIC) adv_norm(stats, m_global, meanf, stdf);
+  const double inv_m = uniform_d(1.0 / m_global);
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+  tile_loop<KIND>(ws, gw, nw, M, X, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
+    p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
+  });
+  p.finish(ws, gpart + (size_t)gw * NWP, dpart + gw * 3);
+}
+
+// Actor pass of epoch e fused with the critic pass of epoch e + 1 (Algo_PPO.train_model_c
+// :778-815 run as a pipeline: the actor of epoch e needs only V_e and the advantage sums of the
+// critic pass e; the critic of epoch e + 1 needs only the critic's Adam step e).  Both nets
+// train on the same tile: one input load, one launch and one weight-staging prologue instead of
+// two.  The actor reads V_e from the tile's prefetched inputs before the critic overwrites those
+// rows of V with V_{e+1} (each tile belongs to one wave; its inputs land one tile ahead).
+// Partials: actor at gpart[gw], critic at gpart[nw + gw] (and dpart likewise).
+#ifndef MHPPO_PAIR_HB
+#define MHPPO_PAIR_HB false
+#endif
+constexpr bool PAIR_HB = MHPPO_PAIR_HB;
+__global__ void __launch_bounds__(64 * x3::WAVES)
+    k_mlp_train_x3_pair(const float *__restrict__ Wa, const float *__restrict__ Wc, const float *__restrict__ X,
+                        int64_t M, const float *__restrict__ ret, float *__restrict__ V,
+                        const float *__restrict__ act, const float *__restrict__ lp_old,
+                        const double *__restrict__ stats, double m_global, float out_mean, float out_std,
+                        float *__restrict__ gpart, double *__restrict__ dpart) {
+  using namespace x3;
+  extern __shared__ float lds[];
+  char *L8 = reinterpret_cast<char *>(lds);
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  stage_net(Wa, L8, tid);
+  stage_net(Wc, L8 + NET_B, tid);
+  __syncthreads();
+  const WaveSlot ws(L8 + 2 * NET_B, w, l);
+  Pass<K_CONT, false, PAIR_HB> pa;
+  Pass<K_CRITIC, false, PAIR_HB> pc;
+  pa.init(L8, ws);
+  pc.init(L8 + NET_B, ws);
+  float meanf, stdf;
+  adv_norm(stats, m_global, meanf, stdf);
+  const double inv_m = uniform_d(1.0 / m_global);
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+  tile_loop<K_CONT>(ws, gw, nw, M, X, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
+    pa.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
+    pc.tile(ws, slot, row0, nrows, V, 0.f, 1.f, inv_m, out_mean, out_std);
+  });
+  pa.finish(ws, gpart + (size_t)gw * NWP, dpart + gw * 3);
+  pc.finish(ws, gpart + (size_t)(nw + gw) * NWP, dpart + (nw + gw) * 3);
 }
 
 
@@ -1399,10 +1525,15 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
 // Slot k < np is gradient k, slots np..np+2 the float64 sums.
 constexpr int RG = 64;
 
+// blockIdx.z = net: a fused pair launch reduces both nets' partials (net z's waves follow net
+// z - 1's in gpart / dpart; its group totals at tmp + z RG (np + 3)) in the same two launches.
 __global__ void __launch_bounds__(256)
     k_grad_stage1(const float *gpart, const double *dpart, int nw, int np, double *tmp) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  const int g = blockIdx.y, nd = np + 3;
+  const int g = blockIdx.y, nd = np + 3, z = blockIdx.z;
+  gpart += (size_t)z * nw * np;
+  dpart += (size_t)z * nw * 3;
+  tmp += (size_t)z * RG * nd;
   const int i0 = (int)((int64_t)g * nw / RG), i1 = (int)((int64_t)(g + 1) * nw / RG);
   double s = 0.0;
   if (k < np) {
@@ -1417,9 +1548,15 @@ __global__ void __launch_bounds__(256)
   tmp[(size_t)g * nd + k] = s;
 }
 
-__global__ void __launch_bounds__(256) k_grad_stage2(const double *tmp, int np, float *grad, double *out3) {
+__global__ void __launch_bounds__(256)
+    k_grad_stage2(const double *tmp, int np, float *grad, double *out3, float *grad1, double *out3_1) {
   const int k = blockIdx.x * 256 + threadIdx.x, nd = np + 3;
   if (k >= nd) return;
+  if (blockIdx.z) {
+    tmp += (size_t)RG * nd;
+    grad = grad1;
+    out3 = out3_1;
+  }
   double s = 0.0;
 #pragma unroll 8
   for (int g = 0; g < RG; g++) s += tmp[(size_t)g * nd + k];
@@ -1437,6 +1574,30 @@ struct Work {  // per-device partial buffers (calls on one device must share one
   int cus = 0;
 };
 Work g_work[mhppo::MAX_DEVICES];
+// partial buffers for `slots` waves' partials (a fused pair launch uses two slots per wave)
+bool ensure_work(Work &wk, int slots) {
+  if (wk.nw >= slots) return true;
+  if (wk.g) (void)hipFree(wk.g);
+  if (wk.d) (void)hipFree(wk.d);
+  if (wk.t) (void)hipFree(wk.t);
+  if (hipMalloc(&wk.g, sizeof(float) * (size_t)slots * NW_MAX) != hipSuccess ||
+      hipMalloc(&wk.d, sizeof(double) * (size_t)slots * 3) != hipSuccess ||
+      hipMalloc(&wk.t, sizeof(double) * (size_t)2 * RG * (NW_MAX + 3)) != hipSuccess) {
+    wk = Work{};
+    return false;
+  }
+  wk.nw = slots;
+  return true;
+}
+Work &device_work(int dev) {
+  Work &wk = g_work[dev];
+  if (wk.cus == 0) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    wk.cus = cus;
+  }
+  return wk;
+}
 
 template <int KIND, int KS, bool PF>
 void launch(dim3 grid, hipStream_t s, const float *packed, const float *X, int nin, int64_t M, const float *ret,
@@ -1483,30 +1644,14 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   int dev = 0;
   CHECK_HIP(hipGetDevice(&dev));
   if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
-  Work &wk = g_work[dev];
-  if (wk.cus == 0) {
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    wk.cus = cus;
-  }
+  Work &wk = device_work(dev);
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
   const int waves = split ? x3::WAVES : (pf ? 8 : 4);
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
   const int64_t tiles = (M + 31) / 32;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
   const int nw = (int)blocks * waves;
-  if (wk.nw < nw) {
-    if (wk.g) (void)hipFree(wk.g);
-    if (wk.d) (void)hipFree(wk.d);
-    if (wk.t) (void)hipFree(wk.t);
-    if (hipMalloc(&wk.g, sizeof(float) * (size_t)nw * NW_MAX) != hipSuccess ||
-        hipMalloc(&wk.d, sizeof(double) * (size_t)nw * 3) != hipSuccess ||
-        hipMalloc(&wk.t, sizeof(double) * (size_t)RG * (NW_MAX + 3)) != hipSuccess) {
-      wk = Work{};
-      return set_error(MHPPO_ENOMEM, "mlp_train partials");
-    }
-    wk.nw = nw;
-  }
+  if (!ensure_work(wk, nw)) return set_error(MHPPO_ENOMEM, "mlp_train partials");
   const dim3 grid((unsigned)blocks);
 #define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
   if (split) {
@@ -1543,7 +1688,44 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
 #undef MLP_ARGS
   const int np = n_params(n_in, kind == K_CHOICE ? 2 : 1);
   hipLaunchKernelGGL(k_grad_stage1, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, np, wk.t);
-  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums);
+  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums, nullptr,
+                     nullptr);
+  CHECK_HIP(hipGetLastError());
+  return MHPPO_OK;
+}
+
+extern "C" int mhppo_mlp_train_pair(const float *packed_actor, const float *packed_critic, const float *X, int64_t M,
+                                    const float *ret, float *value, const float *act, const float *logp_old,
+                                    const double *stats, double m_global, float out_mean, float out_std,
+                                    float *grad_actor, double *sums_actor, float *grad_critic, double *sums_critic,
+                                    void *stream) {
+  if (!grad_actor || !grad_critic || M < 0) return set_error(MHPPO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int np = n_params(NIN_CONT, 1);
+  if (M == 0) {  // an empty shard: zero gradients, sums unchanged
+    CHECK_HIP(hipMemsetAsync(grad_actor, 0, sizeof(float) * np, s));
+    CHECK_HIP(hipMemsetAsync(grad_critic, 0, sizeof(float) * np, s));
+    return MHPPO_OK;
+  }
+  if (!packed_actor || !packed_critic || !X || !ret || !value || !act || !logp_old || !stats)
+    return set_error(MHPPO_EINVAL, "null pointer");
+  if (M > ((int64_t)1 << 40)) return set_error(MHPPO_EINVAL, "M too large");
+  if (((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
+  Work &wk = device_work(dev);
+  const int64_t tiles = (M + 31) / 32;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(wk.cus, (tiles + x3::WAVES - 1) / x3::WAVES));
+  const int nw = (int)blocks * x3::WAVES;
+  if (!ensure_work(wk, 2 * nw)) return set_error(MHPPO_ENOMEM, "mlp_train partials");
+  hipLaunchKernelGGL(k_mlp_train_x3_pair, dim3((unsigned)blocks), dim3(64 * x3::WAVES), x3::LDS_BYTES_PAIR, s,
+                     packed_actor, packed_critic, X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std,
+                     wk.g, wk.d);
+  // the two nets' partials (actor waves [0, nw), critic waves [nw, 2 nw)) in one launch pair
+  hipLaunchKernelGGL(k_grad_stage1, dim3((np + 3 + 255) / 256, RG, 2), dim3(256), 0, s, wk.g, wk.d, nw, np, wk.t);
+  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256, 1, 2), dim3(256), 0, s, wk.t, np, grad_actor,
+                     sums_actor, grad_critic, sums_critic);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

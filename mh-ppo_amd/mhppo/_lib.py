@@ -90,6 +90,7 @@ _SIGS = {
     "mhppo_ppo_choice_fwd_bwd": (I32, [P, P, P, I64, P, F64, P, P, P]),
     "mhppo_mse_fwd_bwd": (I32, [P, P, I64, F64, P, P, P]),
     "mhppo_mlp_train": (I32, [I32, I32, P, P, I64, P, P, P, P, P, P, F64, ctypes.c_float, ctypes.c_float, P, P, P]),
+    "mhppo_mlp_train_pair": (I32, [P, P, P, I64, P, P, P, P, P, F64, ctypes.c_float, ctypes.c_float, P, P, P, P, P]),
     "mhppo_last_error": (ctypes.c_char_p, []),
     "mhppo_version": (ctypes.c_char_p, []),
 }

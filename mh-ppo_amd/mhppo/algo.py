@@ -139,8 +139,10 @@ class Algo_PPO:
                     dist.broadcast(p.data, src=0)
         # every net's flat gradient in one contiguous buffer: one in-place all-reduce per
         # joint epoch under data parallelism (mhppo.ppo.GradBucket)
-        self.grad_bucket = ppo.GradBucket([self.actor_net_cross, self.critic_net_cross, self.actor_net_wait,
-                                           self.critic_net_wait, self.actor_net_choice, self.critic_net_choice],
+        # (actors first, then critics: the first and last steps of the epoch pipeline, which train
+        # only the critics / only the actors, reduce one contiguous span too)
+        self.grad_bucket = ppo.GradBucket([self.actor_net_cross, self.actor_net_wait, self.actor_net_choice,
+                                           self.critic_net_cross, self.critic_net_wait, self.critic_net_choice],
                                           dev)
         # one fused Adam launch per net and step on the GPU (the reference's default Adam
         # semantics: lr, betas (0.9, 0.999), eps 1e-8, no weight decay)
@@ -229,9 +231,7 @@ class Algo_PPO:
                                       self.optimizer_critic_choice, d["obs"], d["act"], d["logp"], d["ret"], m_d,
                                       counts, per_row=self.fix_choice_loss))
                 names.append("choice")
-            losses = None
-            for _ in range(10):
-                losses = ppo.train_epoch(heads, self.grad_bucket)
+            losses = ppo.train_epochs(heads, 10, self.grad_bucket) if heads else None
         if self.verbose and losses is not None:
             div = {"cross": (m_c, m_c), "wait": (m_w, m_w), "choice": (m_d * m_d, m_d)}
             if self.fix_choice_loss:

@@ -26,6 +26,8 @@ gradient is that of (global-mean loss restricted to its rows), so the reduced
 gradient is the full-batch gradient; Adam then runs replicated.  A rank whose shard
 of a head is empty still joins both collectives (the kernel writes a zero gradient).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -247,6 +249,40 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     return grad, sums, (V if kind == KIND_CRITIC else None)
 
 
+def k_mlp_train_pair(actor, critic, obs, ret, value, act, logp_old, stats, m_global, sums_actor, sums_critic):
+    """Actor pass of epoch e + critic pass of epoch e + 1 of one continuous head in one launch
+    (mhppo_mlp_train_pair): `value` holds V_e (the critic pass e's outputs) and is overwritten
+    with V_{e+1}; `stats` are the critic pass e's global advantage sums; the critic's weights
+    must already carry its Adam step e.  Gradients go to both nets' flat .grad storage; the
+    float64 sums accumulate into sums_actor / sums_critic (zeroed [3] each)."""
+    for net, kind in ((actor, 1), (critic, 0)):
+        if net.model_type != kind or net.n_in != 13 or net.n_out != 1:
+            raise ValueError("the fused pair launch trains a 13 -> 1 continuous actor and its 13 -> 1 critic")
+    dev = obs.device
+    M = obs.shape[0]
+    obs = obs.float().contiguous()
+    if obs.data_ptr() % 16:
+        obs = obs.clone()
+    ret, act, logp_old = ret.float().contiguous(), act.float().contiguous(), logp_old.float().contiguous()
+    if value.dtype != torch.float32 or not value.is_contiguous() or value.numel() != M:
+        raise ValueError("value must be the float32 [M] buffer of the previous critic pass (updated in place)")
+    ga, gc = actor.grad_flat(), critic.grad_flat()
+    p = _lib.ptr
+    ev = None
+    if TRAIN_EVENTS is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().mhppo_mlp_train_pair(
+            p(actor.flat()), p(critic.flat()), p(obs), M, p(ret), p(value), p(act), p(logp_old), p(stats),
+            float(m_global), float(actor.mean), float(actor.std), p(ga), p(sums_actor), p(gc), p(sums_critic),
+            _lib.stream_ptr()))
+    if ev is not None:
+        ev[1].record()
+        TRAIN_EVENTS.append((3, 13, M, ev[0], ev[1]))  # kind 3: a fused pair launch (two passes)
+    return ga, gc, value
+
+
 # ------------------------------------------------------------- DP orchestration
 
 class Head:
@@ -297,6 +333,66 @@ def train_epoch(heads, bucket=None):
     return out
 
 
+# Fuse each continuous head's actor pass e with its critic pass e + 1 (train_epochs).  Off: every
+# pass is its own launch, as train_epoch runs it.  MHPPO_PIPELINE_PAIRS=0 turns it off (A/B).
+PIPELINE_PAIRS = os.environ.get("MHPPO_PIPELINE_PAIRS", "1") != "0"
+
+
+def train_epochs(heads, n_epochs, bucket=None):
+    """n_epochs full-batch epochs of every head, run as a pipeline of n_epochs + 1 steps: step k
+    runs the actor passes of epoch k - 1 and the critic passes of epoch k (a continuous head on the
+    split-precision kernel: ONE fused launch, mhppo_mlp_train_pair), then one gradient all-reduce
+    of the nets trained in the step, one all-reduce of the new critic passes' advantage sums and
+    the Adam steps.  The same arithmetic as n_epochs calls of train_epoch: the actor of epoch e
+    uses V_e and the advantage sums of the critic pass e (critic weights of epoch e), the critic
+    of epoch e + 1 the critic's weights after its Adam step e; each optimiser steps n_epochs
+    times.  Returns this rank's (actor, critic) loss sums of the last epoch per head."""
+    H = len(heads)
+    dev = heads[0].obs.device
+    paired = [PIPELINE_PAIRS and h.kind == "c" and not h.exact for h in heads]
+    V = [None] * H      # V_e of each head (a paired head's buffer is updated in place)
+    stats = None        # all-reduced advantage sums of the previous step's critic passes [2H]
+    out = [[None, None] for _ in range(H)]
+    for k in range(n_epochs + 1):
+        sums = torch.zeros(2 * H, 3, dtype=torch.float64, device=dev)  # critic rows, actor rows
+        crit = k < n_epochs
+        trained = []
+        for i, h in enumerate(heads):
+            sc, sa = sums[i], sums[H + i]
+            st = stats[2 * i:2 * i + 2] if k > 0 else None
+            if k > 0 and crit and paired[i]:
+                k_mlp_train_pair(h.actor, h.critic, h.obs, h.ret, V[i], h.act, h.logp, st, h.m, sa, sc)
+                trained += [h.actor, h.critic]
+                out[i] = [sa[0:1], sc[0:1]]
+                continue
+            if k > 0:  # the actor pass of epoch k - 1
+                if h.kind == "c":
+                    k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V[i], h.act, h.logp, st, m_global=h.m, sums=sa,
+                                exact=h.exact)
+                elif h.per_row:
+                    k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], h.act.float(), h.logp, st, None,
+                                m_global=h.m, sums=sa)
+                else:
+                    k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], None, h.logp, st, h.counts, m_global=h.m,
+                                sums=sa)
+                trained.append(h.actor)
+                out[i][0] = sa[0:1]
+            if crit:  # the critic pass of epoch k
+                _, _, V[i] = k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sc, exact=h.exact)
+                trained.append(h.critic)
+                out[i][1] = sc[0:1]
+        if crit:
+            stats = sums[:H, 1:3].reshape(-1).contiguous()
+            _allreduce_(stats)
+        if bucket is not None:
+            bucket.allreduce(trained)
+        else:
+            _allreduce_net_grads(*trained)
+        adam_steps([h.opt_actor for h in heads if h.actor in trained] +
+                   [h.opt_critic for h in heads if h.critic in trained])
+    return [tuple(o) for o in out]
+
+
 def _no_step_hooks(o):
     """No optimizer step hooks (per instance or global): the fast path bypasses Optimizer.step."""
     from torch.optim import optimizer as _opt
@@ -314,6 +410,32 @@ def _fused_adam_ok(o):
                     for g in o.param_groups))
 
 
+class _AdamPlan:
+    """The grouped tensor lists of one adam_steps(opts) call, reused while every optimiser keeps
+    the same state / param_groups objects, hyper-parameters and .grad tensors (an optimiser's
+    load_state_dict replaces those objects; a rebound .grad is a different tensor)."""
+
+    def __init__(self, opts, keys, groups, steps, grads):
+        self.opts, self.keys, self.groups, self.steps = opts, keys, groups, steps
+        self.ids = [(id(o.state), id(o.param_groups)) for o in opts]
+        self.grads = grads  # [(param, grad)]
+
+    def valid(self, opts):
+        if [(id(o.state), id(o.param_groups)) for o in opts] != self.ids:
+            return False
+        if _group_keys(opts) != self.keys or not all(_no_step_hooks(o) for o in opts):
+            return False
+        return all(p.grad is g for p, g in self.grads)
+
+
+def _group_keys(opts):
+    return [(float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["weight_decay"]), float(g["eps"]),
+             bool(g["maximize"])) for o in opts for g in o.param_groups]
+
+
+_ADAM_PLANS = {}
+
+
 def adam_steps(opts):
     """One step of every optimiser in `opts`, bit-identical to calling o.step() on each.  For
     fused torch Adams (the GPU path) whose state exists, the steps of all six nets run as ONE
@@ -324,9 +446,16 @@ def adam_steps(opts):
     hooks, a torch without the private torch._fused_adam_ op) takes o.step().  The fast path
     reads each group's lr at every call, so an LR scheduler's changes apply; it does not run
     Optimizer.step itself (no step hooks — hence the fallback above — and no scheduler
-    step-order bookkeeping).  Pinned by test_adam_steps_bit_identical_to_per_optimizer_steps."""
+    step-order bookkeeping).  The grouped tensor lists are built once per optimiser set and
+    reused (_AdamPlan: ~0.2 ms of host time per call otherwise).  Pinned by
+    test_adam_steps_bit_identical_to_per_optimizer_steps."""
+    key = tuple(id(o) for o in opts)
+    plan = _ADAM_PLANS.get(key)
+    if plan is not None and plan.opts == list(opts) and plan.valid(opts):
+        _run_adam_plan(plan)
+        return
     fast = all(_fused_adam_ok(o) for o in opts)
-    groups, steps = {}, []
+    groups, steps, grads = {}, [], []
     if fast:
         for o in opts:
             for g in o.param_groups:
@@ -336,12 +465,12 @@ def adam_steps(opts):
                     break
                 if not ps:
                     continue
-                key = (ps[0].device, float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]),
-                       float(g["weight_decay"]), float(g["eps"]), bool(g["maximize"]))
-                e = groups.setdefault(key, ([], [], [], [], []))
+                hk = (ps[0].device, float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]),
+                      float(g["weight_decay"]), float(g["eps"]), bool(g["maximize"]))
+                e = groups.setdefault(hk, ([], [], [], [], []))
                 for p in ps:
                     st = o.state[p]
-                    if p.dtype != torch.float32 or p.device != key[0]:
+                    if p.dtype != torch.float32 or p.device != hk[0]:
                         fast = False
                     e[0].append(p)
                     e[1].append(p.grad)
@@ -349,14 +478,24 @@ def adam_steps(opts):
                     e[3].append(st["exp_avg_sq"])
                     e[4].append(st["step"])
                     steps.append(st["step"])
+                    grads.append((p, p.grad))
             if not fast:
                 break
     if not fast:
+        _ADAM_PLANS.pop(key, None)
         for o in opts:
             o.step()
         return
-    torch._foreach_add_(steps, 1)
-    for (_, lr, b1, b2, wd, eps, maximize), (ps, gs, ms, vs, sts) in groups.items():
+    plan = _AdamPlan(list(opts), _group_keys(opts), groups, steps, grads)
+    if len(_ADAM_PLANS) > 64:
+        _ADAM_PLANS.clear()
+    _ADAM_PLANS[key] = plan
+    _run_adam_plan(plan)
+
+
+def _run_adam_plan(plan):
+    torch._foreach_add_(plan.steps, 1)
+    for (_, lr, b1, b2, wd, eps, maximize), (ps, gs, ms, vs, sts) in plan.groups.items():
         torch._fused_adam_(ps, gs, ms, vs, [], sts, amsgrad=False, lr=lr, beta1=b1, beta2=b2, weight_decay=wd,
                            eps=eps, maximize=maximize, grad_scale=None, found_inf=None)
 

@@ -91,8 +91,16 @@ def _install_cpu_doubles(ppo):
         gf.copy_(torch.cat([(x if x is not None else torch.zeros_like(q)).reshape(-1) for x, q in zip(g, params)]))
         return gf, torch.cat([loss, torch.zeros(2, dtype=torch.float64)]), None
 
+    def mlp_train_pair(actor, critic, obs, ret, value, act, lp_old, stats, m_global, sums_a, sums_c):
+        """mhppo_mlp_train_pair's contract: actor pass e on V_e, then critic pass e + 1 into value."""
+        mlp_train(1, actor, obs, ret, value, act, lp_old, stats, m_global=m_global, sums=sums_a)
+        _, _, v = mlp_train(0, critic, obs, ret, m_global=m_global, sums=sums_c)
+        value.copy_(v)
+        return actor.grad_flat(), critic.grad_flat(), value
+
     ppo.k_adv_stats, ppo.k_adv_normalize, ppo.k_mse, ppo.k_ppo_cont = adv_stats, adv_normalize, mse, ppo_cont
     ppo.k_mlp_train = mlp_train
+    ppo.k_mlp_train_pair = mlp_train_pair
 
 
 def _run(rank, world, port, data, out_q):

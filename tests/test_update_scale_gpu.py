@@ -90,3 +90,65 @@ def test_fused_epoch_at_bench_scale_vs_float64_autograd(exact):
     g64 = _flat_grad(a64, surr.sum() / m)
     assert float((ga.double() - g64).abs().max()) <= 1e-4 * float(g64.abs().max())
     assert abs(float(sa[0]) - float(surr.sum())) <= 1e-6 * float(surr.abs().sum())
+
+
+def _pair_vs_passes(critic, actor, obs, ret, act, lp, m):
+    """One fused pair launch against the actor pass e and the critic pass e + 1 run as two
+    launches on the same inputs: gradients, sums and V_{e+1} must be bit-identical."""
+    from mhppo import ppo
+    _, sc0, V0 = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+    stats = sc0[1:3].clone()
+    with torch.no_grad():  # the critic's Adam step e (any update of its weights)
+        for prm in critic.parameters():
+            prm.add_(torch.randn_like(prm) * 1e-3)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, V0, act, lp, stats, m_global=m)
+    ga, sa = ga.clone(), sa.clone()
+    gc, sc, V1 = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+    gc, sc = gc.clone(), sc.clone()
+    V = V0.clone()
+    sa2 = torch.zeros(3, dtype=torch.float64, device=obs.device)
+    sc2 = torch.zeros(3, dtype=torch.float64, device=obs.device)
+    ga2, gc2, V = ppo.k_mlp_train_pair(actor, critic, obs, ret, V, act, lp, stats, m, sa2, sc2)
+    assert torch.equal(ga2, ga) and torch.equal(gc2, gc)
+    assert torch.equal(V, V1)
+    assert torch.equal(sa2, sa) and torch.equal(sc2, sc)
+
+
+def test_pair_launch_bit_identical_to_two_passes():
+    """mhppo_mlp_train_pair (actor pass e + critic pass e + 1 in one launch) on the bench's real
+    10.5 M-row bucket and on a ragged 70 001-row slice of it."""
+    from mhppo.algo import Algo_PPO
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import bucket_segments
+    venv = VecCrosswalk("4cars", 65536, 4, 1, 2, seed_base=0)
+    torch.manual_seed(0)
+    algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
+    with torch.no_grad():
+        batch = algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0)
+    c, _, _ = bucket_segments(batch)
+    obs, act, lp, ret = c["obs"], c["act"], c["logp"], c["ret"]
+    for n in (obs.shape[0], 70001):
+        _pair_vs_passes(algo.critic_net_cross, algo.actor_net_cross, obs[:n], ret[:n], act[:n], lp[:n], float(n))
+
+
+def test_pipelined_epochs_equal_sequential():
+    """Algo_PPO.update's pipelined epochs (ppo.train_epochs: actor e fused with critic e + 1) train
+    bit-identical nets to the epoch-by-epoch schedule (PIPELINE_PAIRS off: every pass its own
+    launch, the same order of Adam steps per optimiser)."""
+    from mhppo import ppo
+    from mhppo.algo import Algo_PPO
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    nets = []
+    try:
+        for pipe in (True, False):
+            ppo.PIPELINE_PAIRS = pipe
+            venv = VecCrosswalk("4cars", 2048, 4, 1, 2, seed_base=5)
+            torch.manual_seed(0)
+            algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=1, save_curves=False)
+            algo.train(2)
+            nets.append(torch.cat([n.flat() for n in algo.nets()]).cpu())
+    finally:
+        ppo.PIPELINE_PAIRS = True
+    assert torch.equal(nets[0], nets[1])

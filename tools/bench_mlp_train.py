@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10485760)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--exact", action="store_true", help="the exact f32-MFMA kernel (MHPPO_TRAIN_EXACT_F32)")
+ap.add_argument("--pair", action="store_true", help="also time the fused actor+critic launch (mhppo_mlp_train_pair)")
 a = ap.parse_args()
 M = a.rows
 torch.manual_seed(0)
@@ -40,4 +41,18 @@ for kind in (0, 1):
     tf = ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12
     print(f"kind {kind} rows {M}: {ms:.3f} ms  {tf:.1f} TFLOP/s "
           f"({100 * tf / 157.3:.1f}% of f32 MFMA peak)", flush=True)
+if a.pair:
+    V2 = V.clone()
+    sa2, sc2 = (torch.zeros(3, dtype=torch.float64, device="cuda") for _ in range(2))
+    st = sc[1:3].clone()
+    for _ in range(2):
+        ppo.k_mlp_train_pair(actor, critic, obs, ret, V2, act, lp, st, float(M), sa2, sc2)
+    torch.cuda.synchronize()
+    ppo.TRAIN_EVENTS = []
+    for _ in range(a.reps):
+        ppo.k_mlp_train_pair(actor, critic, obs, ret, V2, act, lp, st, float(M), sa2, sc2)
+    torch.cuda.synchronize()
+    ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
+    tf = 2 * ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12
+    print(f"pair rows {M}: {ms:.3f} ms (both passes)  {tf:.1f} TFLOP/s", flush=True)
 ppo.TRAIN_EVENTS = None

@@ -7,8 +7,9 @@ destination registers to the compiler as if the data were ready; the next block 
 allocator leaves those VGPRs untouched until that wait: a v_mov copy, a spill or a
 rematerialisation in between would read (or clobber) registers whose LDS data is still in
 flight and silently corrupt the weight gradients.  This script checks the invariant on the
-code object actually built: for every ds_read_b64_tr_b16 issued right after an MFMA (the
-in-gap reads; the compiler's own reads are waited for by its own counters), no instruction
+code object actually built: for every in-gap ds_read_b64_tr_b16 (the asm blocks' runs of six
+(AGPR-accumulating MFMA, read) pairs; the compiler's own reads are waited for by its own
+counters), no instruction
 may read or write any of its destination VGPRs before the next s_waitcnt lgkmcnt(0), and no
 branch or label may intervene.
 
@@ -66,13 +67,22 @@ def parse(line):
 def check_function(name, lines):
     """Violations in one kernel's disassembly (list of strings)."""
     bad, n_reads = [], 0
-    insts = [(ln, parse(ln)) for ln in lines]
+    insts = [(ln, p) for ln, p in ((ln, parse(ln)) for ln in lines)]
+    ops = [(i, p) for i, (ln, p) in enumerate(insts) if p]
+
+    def agpr_mfma(p):
+        return p[0].startswith("v_mfma") and p[1][0].startswith("a[")
+
+    # The asm blocks are runs of six (MFMA accumulating in AGPRs, ds_read_b64_tr_b16) pairs.  The
+    # compiler's own MFMAs in this translation unit write VGPRs (-amdgpu-mfma-vgpr-form) and its
+    # own LDS reads are covered by its own counted waits.
+    asm_reads = set()
+    for n in range(len(ops) - 11):
+        if all(agpr_mfma(ops[n + 2 * q][1]) and ops[n + 2 * q + 1][1][0] == "ds_read_b64_tr_b16" for q in range(6)):
+            asm_reads.update(ops[n + 2 * q + 1][0] for q in range(6))
     for k, (ln, pi) in enumerate(insts):
-        if not pi or pi[0] != "ds_read_b64_tr_b16":
+        if k not in asm_reads:
             continue
-        prev = next((q for q in reversed(insts[:k]) if q[1]), None)
-        if prev is None or not prev[1][0].startswith("v_mfma"):
-            continue  # a compiler-placed read: its own counters cover it
         n_reads += 1
         pending = regs(pi[1][0])
         for ln2, p2 in insts[k + 1:]:

@@ -20,6 +20,38 @@ PHASES = {1: "MT refill (wave)", 2: "env state load (EnvR)", 3: "select + MVN ac
           12: "observe: ped get_data", 8: "observe: obs block store", 9: "commit", 10: "rollout buffer writes"}
 
 
+def per_step(algo, fn, buf):
+    """Phase cycles per wave of every step of one rollout (the collect loop of RolloutGPU.collect,
+    synchronised and read back after each env-step launch)."""
+    L = _lib.lib()
+    ro = algo.rollout.gpu
+    algo.rollout.reset()
+    with torch.no_grad():
+        ro.draw_noise(0, 2)
+        mc, tc = algo.actor_net_choice.mlp_desc()
+        mx, tx = algo.actor_net_cross.mlp_desc()
+        mw, tw = algo.actor_net_wait.mlp_desc()
+        st = _lib.stream_ptr()
+        _lib.check(L.mhppo_rollout_begin(ro.venv.handle, ctypes.byref(mc), _lib.ptr(ro.u), None, ctypes.byref(ro._bufs),
+                                         st))
+        rows = []
+        for t in range(ro.T):
+            if ro.P == 1:
+                ro._bufs.feat_c = ro.obs_c[t].data_ptr()
+            _lib.check(L.mhppo_rollout_policy(ro.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                              ctypes.byref(ro._bufs), st))
+            torch.cuda.synchronize()
+            fn(buf)  # clears
+            _lib.check(L.mhppo_rollout_sample_env(ro.venv.handle, _lib.ptr(ro.eps[t]), t, ctypes.byref(ro._bufs), st))
+            torch.cuda.synchronize()
+            fn(buf)
+            w = max(buf[15], 1)
+            rows.append([buf[k] / w for k in PHASES])
+    print("step " + " ".join(f"{PHASES[k][:10]:>10s}" for k in PHASES))
+    for t, r in enumerate(rows):
+        print(f"{t:4d} " + " ".join(f"{x:10.0f}" for x in r) + f"  total {sum(r):8.0f}")
+
+
 def main():
     v, nc, npd, nl, N = (sys.argv[1:2] or ["4cars"])[0], *map(int, (sys.argv[2:6] or [4, 1, 2, 65536]))
     venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=0)
@@ -41,6 +73,8 @@ def main():
         ev[1].record()
         torch.cuda.synchronize()
         fn(buf)
+    if os.environ.get("PER_STEP"):  # one more iteration, phases read back after every step
+        per_step(algo, fn, buf)
     waves = buf[15]
     tot = sum(buf[k] for k in PHASES)
     print(f"{v} {nc}/{npd}/{nl} N={N}: {waves} wave-launches, collect {ev[0].elapsed_time(ev[1]):.2f} ms")
