@@ -481,5 +481,12 @@ inline void build_cfg(const mhppo_env_cfg &cfg_, Cfg &c) {
   c.seed_base = cfg->seed_base;
   c.env_off = cfg->env_id_offset;
   c.flags = cfg->flags;
+  c.tb = -(10.0 / (2.0 * c.b00)) + 1.;  // (:564) as the device computed it per call
+  {
+    const double d = -2.0 * c.b00;
+    int e = 0;
+    c.brake_p2 = d > 0.0 && frexp(d, &e) == 0.5;  // d = 2^(e-1): 1 / d is exact
+    c.brake_inv = c.brake_p2 ? 1.0 / d : 0.0;
+  }
 }
 }  // namespace mhppo

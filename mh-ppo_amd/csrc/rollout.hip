@@ -551,16 +551,32 @@ __global__ void __launch_bounds__(TPB)
 
 // No MT refill in the register-view step kernel: the episode's reset kernel regenerated every stale block
 // (see k_policy_mfma), and a block exhausted twice within one episode is twisted in-lane by RngT
+#ifdef MHPPO_WAVE_TIMES
+// A/B builds only (tools/env_waves.py): each wave's shader-clock start / end of the last launch
+__device__ unsigned long long g_wave_times[2 * 8192];
+#endif
 template <int V, int NC, int NAV, int NP>
 __global__ void __launch_bounds__(TPB)
     k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
   const int e = blockIdx.x * TPB + threadIdx.x;
+#ifdef MHPPO_WAVE_TIMES
+  const unsigned long long wt0 = __builtin_amdgcn_s_memtime();
+#endif
   MHPPO_MARK(0);
   MHPPO_MARK(1);
   if (e >= c.N) return;
   EnvR<V, NC, NAV, NP> E(c, eb, e);
   MHPPO_MARK(2);
   sample_env_body(E, eps, t, B);
+#ifdef MHPPO_WAVE_TIMES
+  __builtin_amdgcn_s_waitcnt(0);  // the wave's stores issued: it ends here
+  const unsigned long long wt1 = __builtin_amdgcn_s_memtime();
+  const int wv = e >> 6;
+  if ((e & 63) == 0 && wv < 8192) {
+    g_wave_times[2 * wv] = wt0;
+    g_wave_times[2 * wv + 1] = wt1;
+  }
+#endif
 }
 
 // -------------------------------------------------------------- evaluation
@@ -1020,6 +1036,13 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
 
 extern "C" {
 
+#ifdef MHPPO_WAVE_TIMES
+extern "C" int mhppo_debug_wave_times(unsigned long long *out) {  // [2 * 8192]: start, end per wave
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), sizeof(unsigned long long) * 2 * 8192));
+  return MHPPO_OK;
+}
+#endif
 #ifdef MHPPO_TIMING
 // A/B timing builds only (not part of include/mhppo.h): copy out and clear g_timing
 int mhppo_debug_timing(unsigned long long *out16) {

@@ -333,9 +333,21 @@ def train_epoch(heads, bucket=None):
     return out
 
 
-# Fuse each continuous head's actor pass e with its critic pass e + 1 (train_epochs).  Off: every
-# pass is its own launch, as train_epoch runs it.  MHPPO_PIPELINE_PAIRS=0 turns it off (A/B).
-PIPELINE_PAIRS = os.environ.get("MHPPO_PIPELINE_PAIRS", "1") != "0"
+# Fuse each continuous head's actor pass e with its critic pass e + 1 (train_epochs) when the head
+# has at most PAIR_MAX_ROWS rows (global).  The fused launch shares one input load and saves a
+# launch, a weight-staging prologue and a reduction pair per epoch, but with two nets in one wave
+# neither can hold its weight fragments in registers: per tile it is 3.6 % slower than the two
+# passes (profiles/r04_pair/).  Measured end to end: config 2 (328 k rows per head) 7.92 -> 7.53
+# ms per iteration, config 3 (10.5 M rows) 81.9 -> 85.9 ms.  MHPPO_PIPELINE_PAIRS=0 / =1 forces
+# it off / on (A/B).
+PIPELINE_PAIRS = {"0": False, "1": True}.get(os.environ.get("MHPPO_PIPELINE_PAIRS", ""), None)
+PAIR_MAX_ROWS = 2_000_000
+
+
+def _use_pair(h):
+    if h.kind != "c" or h.exact:
+        return False
+    return PIPELINE_PAIRS if PIPELINE_PAIRS is not None else h.m <= PAIR_MAX_ROWS
 
 
 def train_epochs(heads, n_epochs, bucket=None):
@@ -349,7 +361,7 @@ def train_epochs(heads, n_epochs, bucket=None):
     times.  Returns this rank's (actor, critic) loss sums of the last epoch per head."""
     H = len(heads)
     dev = heads[0].obs.device
-    paired = [PIPELINE_PAIRS and h.kind == "c" and not h.exact for h in heads]
+    paired = [_use_pair(h) for h in heads]
     V = [None] * H      # V_e of each head (a paired head's buffer is updated in place)
     stats = None        # all-reduced advantage sums of the previous step's critic passes [2H]
     out = [[None, None] for _ in range(H)]

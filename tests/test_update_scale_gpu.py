@@ -150,5 +150,5 @@ def test_pipelined_epochs_equal_sequential():
             algo.train(2)
             nets.append(torch.cat([n.flat() for n in algo.nets()]).cpu())
     finally:
-        ppo.PIPELINE_PAIRS = True
+        ppo.PIPELINE_PAIRS = None
     assert torch.equal(nets[0], nets[1])

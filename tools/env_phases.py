@@ -46,10 +46,10 @@ def per_step(algo, fn, buf):
             torch.cuda.synchronize()
             fn(buf)
             w = max(buf[15], 1)
-            rows.append([buf[k] / w for k in PHASES])
-    print("step " + " ".join(f"{PHASES[k][:10]:>10s}" for k in PHASES))
-    for t, r in enumerate(rows):
-        print(f"{t:4d} " + " ".join(f"{x:10.0f}" for x in r) + f"  total {sum(r):8.0f}")
+            rows.append(([buf[k] / w for k in PHASES], buf[14]))
+    print("step " + " ".join(f"{PHASES[k][:10]:>10s}" for k in PHASES) + "  (mean wave)   slowest wave")
+    for t, (r, mx) in enumerate(rows):
+        print(f"{t:4d} " + " ".join(f"{x:10.0f}" for x in r) + f"  total {sum(r):8.0f}  max {mx:8d}")
 
 
 def main():
