@@ -202,7 +202,6 @@ def main():
     ppo.TRAIN_EVENTS = []
     # the env-step launches carry HIP events attached to their dispatch packets
     # (hipExtLaunchKernelGGL): the kernel's own execution time, as rocprofv3 reports it
-    _lib.check(L.mhppo_kernel_timing_begin(a.steps * T))
     t0 = time.perf_counter()
     for k in range(a.steps):
         iteration()
@@ -216,10 +215,30 @@ def main():
     dt = float(t.item())
     ms = dt / a.steps * 1e3
     value = world * N * T / (dt / a.steps)
+    # After the timed region (same process, same workload): (1) the env-step kernel over all N envs
+    # with HIP events attached to its 80 launches' dispatch packets (hipExtLaunchKernelGGL: the
+    # kernel's own execution, as rocprofv3 reports it) -> roofline_env; (2) the rollout's wall time
+    # per step (policy + env step) with the one-chain loop and with the product's two-stream parts
+    # (RolloutGPU.parts), from torch events around whole collects.
+    gpu = algo.rollout.gpu
     env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
-    _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(env_ms), ctypes.byref(env_n)))
-    if env_n.value != a.steps * T:
-        raise RuntimeError(f"timed {env_n.value} env-step launches, expected {a.steps * T}")
+    step_us = {}
+    with torch.no_grad():
+        for parts in sorted({1, gpu.parts}):
+            algo.rollout.reset()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if parts == 1:
+                _lib.check(L.mhppo_kernel_timing_begin(T))
+            e0.record()
+            gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=7, iteration=0,
+                        parts=parts)
+            e1.record()
+            torch.cuda.synchronize()
+            if parts == 1:
+                _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(env_ms), ctypes.byref(env_n)))
+            step_us[parts] = e0.elapsed_time(e1) * 1e3 / T
+    if env_n.value != T:
+        raise RuntimeError(f"timed {env_n.value} env-step launches, expected {T}")
     kern_ms = env_ms.value / env_n.value
     S = venv.n_slots
     S_all = 2 * S if variant == "4cars" else S  # car slots incl. the 4cars IDM followers
@@ -228,7 +247,8 @@ def main():
     tr = [e for e in ppo.TRAIN_EVENTS if e[1] == 13]  # the continuous heads' launches
     ppo.TRAIN_EVENTS = None
     tr_ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in tr)
-    tr_rows = sum(m for _, _, m, _, _ in tr)
+    # a fused pair launch (kind 3: actor pass e + critic pass e + 1) runs two passes over its rows
+    tr_rows = sum(m * (2 if k == 3 else 1) for k, _, m, _, _ in tr)
     tr_flops = ppo.FLOPS_PER_ROW_CONT * tr_rows
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     split = not algo.exact_f32
@@ -257,12 +277,17 @@ def main():
                      "frac": tr_tflops / peak, "frac_of_f32_mfma_peak": tr_tflops / F32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic, "traffic_unit": "B/launch",
                      "flops_per_row": ppo.FLOPS_PER_ROW_CONT, "rows_per_launch": tr_rows / max(len(tr), 1),
-                     "launches": len(tr), "launch_ms": tr_ms / max(len(tr), 1)},
+                     "launches": len(tr), "passes": sum(2 if k == 3 else 1 for k, _, _, _, _ in tr),
+                     "launch_ms": tr_ms / max(len(tr), 1)},
         "roofline_env": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_env, "traffic_unit": "B/launch",
                          "bytes_per_launch": per_env * N, "bytes_per_env_step": per_env,
-                         "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3)},
+                         "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3),
+                         "measured_on": "one extra 80-step rollout after the timed region, all N envs per launch"},
+        "rollout_step_us": {"one_chain": step_us[1], "parts": gpu.parts, "product": step_us[gpu.parts],
+                            "note": "wall time per rollout step (policy + env step launches), torch events around "
+                                    "a whole 80-step collect"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)

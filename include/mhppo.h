@@ -154,6 +154,11 @@ typedef struct mhppo_rollout_bufs {
     uint32_t *status;   /* optional device word, zeroed by mhppo_rollout_begin (flags of the current
                            episode only): bit 0 = a NaN choice probability, bit 1 = a NaN continuous
                            action mean was sampled; see mhppo_rollout_check */
+    int32_t parts;      /* 0/1, or P > 1: the envs split in P contiguous parts (boundaries at multiples
+                           of 64 envs) whose steps run as independent chains, e.g. on P streams
+                           (mhppo_rollout_policy_part / _sample_env_part); rows then needs
+                           N*S*P + 2 + 2 (parts + 1) entries */
+    int32_t reserved;
 } mhppo_rollout_bufs;
 /* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
  * instead of the MFMA kernel; both are bit-identical (A/B and tests) */
@@ -203,6 +208,13 @@ int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo
 int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
                          mhppo_rollout_bufs *bufs, void *stream);
 int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
+/* The same two launches for part `part` of bufs->parts only (its envs' rows / its envs): the parts'
+ * step chains are independent, so on separate streams one part's policy MFMA work fills the CUs
+ * another part's latency-bound env step leaves idle.  Results are those of the whole-N calls. */
+int mhppo_rollout_policy_part(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                              mhppo_rollout_bufs *bufs, int part, void *stream);
+int mhppo_rollout_sample_env_part(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, int part,
+                                  void *stream);
 
 /* Measurement (bench.py): the next `n` env-step launches (mhppo_rollout_sample_env) of the
  * calling thread on the device current at this call carry HIP events attached to their dispatch

@@ -282,7 +282,8 @@ __device__ __forceinline__ void stage_both(float *L, const float *__restrict__ W
 template <int V>
 __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__restrict__ Wc,
                                                       const float *__restrict__ Ww, float mean_c, float std_c,
-                                                      float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb) {
+                                                      float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb,
+                                                      int part, int nparts) {
   using namespace pol;
   extern __shared__ float lds[];  // [2][HEAD]: cross, wait
   const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5;
@@ -300,13 +301,23 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
   const int R = c.N * c.nS * c.P;
   const int32_t *__restrict__ rows = B.rows;
   const int nc = __builtin_amdgcn_readfirstlane(rows[R]), nw = __builtin_amdgcn_readfirstlane(rows[R + 1]);
-  const int tc = (nc + 31) / 32, ntiles = tc + (nw + 31) / 32;
+  // this launch's rows: all of both lists, or part `part`'s run of each (k_part_bounds)
+  int c0 = 0, ncp = nc, w0 = nc, nwp = nw;
+  if (nparts > 1) {
+    const int wb = R + 2 + nparts + 1;
+    c0 = __builtin_amdgcn_readfirstlane(rows[R + 2 + part]);
+    ncp = __builtin_amdgcn_readfirstlane(rows[R + 3 + part]) - c0;
+    const int w0r = __builtin_amdgcn_readfirstlane(rows[wb + part]);
+    w0 = nc + w0r;
+    nwp = __builtin_amdgcn_readfirstlane(rows[wb + part + 1]) - w0r;
+  }
+  const int tc = (ncp + 31) / 32, ntiles = tc + (nwp + 31) / 32;
   const ObsLayout L = obs_layout(c);
   // software pipeline over this wave's tiles: row indices two tiles ahead, the rows'
   // observation values one tile ahead, so the gathers overlap the MFMA work
   auto tile_row = [&](int tl, bool &ok) {
     const int hd = tl >= tc;
-    const int a0 = hd ? nc + 32 * (tl - tc) : 32 * tl, a1 = hd ? nc + nw : nc;
+    const int a0 = hd ? w0 + 32 * (tl - tc) : c0 + 32 * tl, a1 = hd ? w0 + nwp : c0 + ncp;
     ok = tl < ntiles && a0 + j < a1;
     return ok ? rows[a0 + j] : 0;
   };
@@ -541,10 +552,10 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
 
 template <int V>
 __global__ void __launch_bounds__(TPB)
-    k_sample_env(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
-  int e = blockIdx.x * TPB + threadIdx.x;
-  mt_refill_wave<TPB / 64>(eb, c.N, e, e < c.N);
-  if (e >= c.N) return;
+    k_sample_env(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B, int e_lo, int e_hi) {
+  int e = e_lo + blockIdx.x * TPB + threadIdx.x;
+  mt_refill_wave<TPB / 64>(eb, c.N, e, e < e_hi);
+  if (e >= e_hi) return;
   Env<V> E(c, eb, e);
   sample_env_body(E, eps, t, B);
 }
@@ -557,14 +568,15 @@ __device__ unsigned long long g_wave_times[2 * 8192];
 #endif
 template <int V, int NC, int NAV, int NP>
 __global__ void __launch_bounds__(TPB)
-    k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B) {
-  const int e = blockIdx.x * TPB + threadIdx.x;
+    k_sample_env_r(Cfg c, Bufs eb, const float *eps, int t, mhppo_rollout_bufs B, int e_lo, int e_hi) {
+  // envs [e_lo, e_hi) (e_lo a multiple of 64: the observation rows leave as whole wave blocks)
+  const int e = e_lo + blockIdx.x * TPB + threadIdx.x;
 #ifdef MHPPO_WAVE_TIMES
   const unsigned long long wt0 = __builtin_amdgcn_s_memtime();
 #endif
   MHPPO_MARK(0);
   MHPPO_MARK(1);
-  if (e >= c.N) return;
+  if (e >= e_hi) return;
   EnvR<V, NC, NAV, NP> E(c, eb, e);
   MHPPO_MARK(2);
   sample_env_body(E, eps, t, B);
@@ -1017,19 +1029,52 @@ inline bool ktime_next(hipEvent_t &a, hipEvent_t &b) {
 // register-view rollout step for a compiled shape (4cars2 has no rollout driver)
 template <int V, int NC, int NAV, int NP>
 bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, const mhppo_rollout_bufs &B,
-                       hipStream_t s) {
+                       hipStream_t s, int e_lo, int e_hi) {
   if constexpr (V == V_4CARS2) {
     return false;
   } else {
     if (!use_reg_view(c, V, NC, NAV, NP)) return false;
-    const dim3 g = grid_for(c.N);
+    const dim3 g = grid_for((size_t)(e_hi - e_lo));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ktime_next(e0, e1))  // same launch, with the timing events attached to its dispatch
-      hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps, t, B);
+      hipExtLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, e0, e1, 0, c, eb, eps, t, B, e_lo,
+                            e_hi);
     else
-      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, c, eb, eps, t, B);
+      hipLaunchKernelGGL((k_sample_env_r<V, NC, NAV, NP>), g, dim3(TPB), 0, s, c, eb, eps, t, B, e_lo, e_hi);
     return true;
   }
+}
+
+// Env range of part `part` of `nparts` (the two-stream rollout, RolloutGPU(parts=2)): boundaries at
+// multiples of 64 envs (whole waves), the last part ends at N
+__host__ __device__ inline int part_env(const Cfg &c, int part, int nparts) {
+  if (part >= nparts) return c.N;
+  const int64_t b = ((int64_t)part * c.N / nparts + 63) / 64 * 64;
+  return (int)std::min<int64_t>(b, c.N);
+}
+
+// Per part, where its rows start in the head lists: rows[R + 2 + p] = cross rows of envs before part
+// p's first env, rows[R + 2 + nparts + 1 + p] = wait rows likewise (p = 0 .. nparts).  The lists
+// are in row order, so a part's rows are one contiguous run of each list (binary search).
+__global__ void k_part_bounds(Cfg c, int32_t *rows, int nparts) {
+  const int p = threadIdx.x;
+  if (p > nparts) return;
+  const int R = c.N * c.nS * c.P, nc = rows[R];
+  const int rb = part_env(c, p, nparts) * c.nS * c.P;
+  int lo = 0, hi = nc;  // first cross index with rows[k] >= rb
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (rows[m] < rb) lo = m + 1;
+    else hi = m;
+  }
+  rows[R + 2 + p] = lo;
+  lo = nc, hi = R;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (rows[m] < rb) lo = m + 1;
+    else hi = m;
+  }
+  rows[R + 2 + nparts + 1 + p] = lo - nc;
 }
 
 }  // namespace
@@ -1059,6 +1104,8 @@ int mhppo_choice_dim(const mhppo_env *env) { return env ? choice_dim(env_cfg(env
 int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const float *u, const int32_t *forced_a,
                         mhppo_rollout_bufs *bufs, void *stream) {
   if (!env || !actor_choice || !bufs || (!u && !forced_a)) return set_error(MHPPO_EINVAL, "null argument");
+  if (bufs->parts < 0 || bufs->parts > 63) return set_error(MHPPO_EINVAL, "parts %d outside [0, 63]", bufs->parts);
+  if (bufs->parts > 1 && !bufs->rows) return set_error(MHPPO_EINVAL, "parts > 1 needs the head lists (rows)");
   GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
   if (actor_choice->n_in != choice_dim(c) || actor_choice->n_out != 2)
@@ -1079,6 +1126,7 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
     if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
     hipLaunchKernelGGL(k_head_count, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt);
     hipLaunchKernelGGL(k_head_place, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt, nblk, bufs->rows);
+    if (bufs->parts > 1) hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, s, c, bufs->rows, (int)bufs->parts);
   }
   size_t NS = (size_t)c.N * c.nS;
   hipLaunchKernelGGL(k_fill_f64, grid_for(NS), dim3(TPB), 0, s, bufs->ep_min, NS, 0.0);  // np.array([0.]*S) (:383)
@@ -1086,8 +1134,26 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
   return MHPPO_OK;
 }
 
+static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                          mhppo_rollout_bufs *bufs, int part, int nparts, void *stream);
+
 int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
                          mhppo_rollout_bufs *bufs, void *stream) {
+  return rollout_policy(env, actor_cross, actor_wait, bufs, 0, 1, stream);
+}
+
+int mhppo_rollout_policy_part(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                              mhppo_rollout_bufs *bufs, int part, void *stream) {
+  if (!bufs) return set_error(MHPPO_EINVAL, "null argument");
+  const int np = bufs->parts > 1 ? bufs->parts : 1;
+  if (part < 0 || part >= np) return set_error(MHPPO_EINVAL, "part %d outside [0, %d)", part, np);
+  if (np > 1 && (bufs->flags & MHPPO_ROLLOUT_VALU_POLICY))
+    return set_error(MHPPO_EINVAL, "parts > 1: MFMA policy only");
+  return rollout_policy(env, actor_cross, actor_wait, bufs, part, np, stream);
+}
+
+static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                          mhppo_rollout_bufs *bufs, int part, int nparts, void *stream) {
   if (!env || !actor_cross || !actor_wait || !bufs) return set_error(MHPPO_EINVAL, "null argument");
   if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
     return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
@@ -1106,11 +1172,12 @@ int mhppo_rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mhp
       cus[dev] = n;
     }
     constexpr size_t WPB = PTPB / 64;  // waves per block
-    const size_t tiles = R / 32 + 2;
-    const size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev], (tiles + WPB - 1) / WPB);
+    const size_t tiles = R / (32 * (size_t)nparts) + 2;
+    const size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev] / nparts + 1,
+                                           (tiles + WPB - 1) / WPB);
     VLAUNCHB(k_policy_mfma, c.variant, dim3((unsigned)blocks), dim3(PTPB), 2 * pol::HEAD * sizeof(float),
              (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std,
-             actor_wait->mean, actor_wait->std, *bufs, env_bufs(env));
+             actor_wait->mean, actor_wait->std, *bufs, env_bufs(env), part, nparts);
     CHECK_HIP(hipGetLastError());
     return MHPPO_OK;
   }
@@ -1179,21 +1246,37 @@ int mhppo_kernel_timing_end_each(float *ms_each, int cap, int *launches) {
   return kernel_timing_collect(nullptr, ms_each, cap, launches);
 }
 
-int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
+static int rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, int part,
+                              int nparts, void *stream) {
   if (!env || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
   if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
   GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
-#define SAMPLE_REG(V_, NC_, NAV_, NP_)                                                   \
-  if (launch_sample_reg<V_, NC_, NAV_, NP_>(c, env_bufs(env), eps, t, *bufs, (hipStream_t)stream)) { \
-    CHECK_HIP(hipGetLastError());                                                        \
-    return MHPPO_OK;                                                                     \
+  const int e_lo = part_env(c, part, nparts), e_hi = part_env(c, part + 1, nparts);
+  if (e_hi <= e_lo) return MHPPO_OK;  // an empty part (N < 64 nparts)
+#define SAMPLE_REG(V_, NC_, NAV_, NP_)                                                                      \
+  if (launch_sample_reg<V_, NC_, NAV_, NP_>(c, env_bufs(env), eps, t, *bufs, (hipStream_t)stream, e_lo, e_hi)) { \
+    CHECK_HIP(hipGetLastError());                                                                           \
+    return MHPPO_OK;                                                                                        \
   }
   MHPPO_REG_SHAPES(SAMPLE_REG)
 #undef SAMPLE_REG
-  VLAUNCH(k_sample_env, c.variant, grid_for(c.N), 0, (hipStream_t)stream, c, env_bufs(env), eps, t, *bufs);
+  VLAUNCH(k_sample_env, c.variant, grid_for((size_t)(e_hi - e_lo)), 0, (hipStream_t)stream, c, env_bufs(env), eps, t,
+          *bufs, e_lo, e_hi);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
+}
+
+int mhppo_rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
+  return rollout_sample_env(env, eps, t, bufs, 0, 1, stream);
+}
+
+int mhppo_rollout_sample_env_part(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, int part,
+                                  void *stream) {
+  if (!bufs) return set_error(MHPPO_EINVAL, "null argument");
+  const int np = bufs->parts > 1 ? bufs->parts : 1;
+  if (part < 0 || part >= np) return set_error(MHPPO_EINVAL, "part %d outside [0, %d)", part, np);
+  return rollout_sample_env(env, eps, t, bufs, part, np, stream);
 }
 
 int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait, const float *eps,

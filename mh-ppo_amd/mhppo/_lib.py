@@ -40,7 +40,7 @@ class RolloutBufs(ctypes.Structure):
     _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
                 ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
                 ("rew", P), ("ep_min", P), ("exist", P), ("rows", P), ("T", I32),
-                ("flags", I32), ("status", P)]
+                ("flags", I32), ("status", P), ("parts", I32), ("reserved", I32)]
 
 
 class EvalBufs(ctypes.Structure):
@@ -71,6 +71,9 @@ _SIGS = {
                                  ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_policy": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
+    "mhppo_rollout_policy_part": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), I32,
+                                        P]),
+    "mhppo_rollout_sample_env_part": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), I32, P]),
     "mhppo_kernel_timing_begin": (I32, [I32]),
     "mhppo_kernel_timing_end": (I32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I32)]),
     "mhppo_kernel_timing_end_each": (I32, [P, I32, ctypes.POINTER(I32)]),

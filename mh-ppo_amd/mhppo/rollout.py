@@ -32,8 +32,23 @@ class RolloutBatch:
         self.__dict__.update(kw)
 
 
+# Envs per part below which the rollout runs as one chain (parts = 1): with fewer than ~256 waves of
+# envs per part the launches are too small for two streams to gain anything
+PART_MIN_ENVS = 16384
+
+
+def default_parts(n_envs, valu_policy=False):
+    """2 (two independent step chains on two streams, RolloutGPU.collect) for large env counts,
+    else 1.  MHPPO_ROLLOUT_PARTS overrides (A/B)."""
+    import os
+    env = os.environ.get("MHPPO_ROLLOUT_PARTS")
+    if env:
+        return max(1, int(env))
+    return 2 if (not valu_policy and n_envs >= 2 * PART_MIN_ENVS) else 1
+
+
 class RolloutGPU:
-    def __init__(self, venv, T=None, valu_policy=False):
+    def __init__(self, venv, T=None, valu_policy=False, parts=None):
         if venv.variant == "4cars2":
             raise ValueError("4cars2 is an env-level variant only: the reference has no driver for it and its "
                              "PPO-driven followers earn no reward (Env_hybrid_multi_coop_4cars2.py:836-847)")
@@ -62,7 +77,11 @@ class RolloutGPU:
         self.exist = z((N, S), torch.uint8)
         self.eps = z((self.T, N, S), f32)
         self.u = z((N, S, P), f32)
-        self.rows = z(N * S * P + 2, i32)  # head-sorted policy rows (filled by mhppo_rollout_begin)
+        self.parts = default_parts(N, valu_policy) if parts is None else int(parts)
+        if self.parts > 1 and valu_policy:
+            raise ValueError("parts > 1 runs the MFMA policy kernel only")
+        # head-sorted policy rows (filled by mhppo_rollout_begin) + the parts' bounds in them
+        self.rows = z(N * S * P + 2 + 2 * (self.parts + 1), i32)
         self.status = z(1, i32)  # NaN flags of the policy draws (mhppo_rollout_check)
         b = _lib.RolloutBufs()
         for name in ("feat_d", "probs_d", "logp_d", "a_d", "closest", "feat_c", "out_c", "obs", "obs_c", "act",
@@ -71,7 +90,10 @@ class RolloutGPU:
         b.T = self.T
         # policy step on the VALU kernel instead of the MFMA one (bit-identical; A/B and tests)
         b.flags = 1 if valu_policy else 0  # MHPPO_ROLLOUT_VALU_POLICY
+        b.parts = self.parts
         self._bufs = b
+        # parts > 1: part p > 0 steps on its own stream (created once), part 0 on the caller's
+        self._side = [torch.cuda.Stream(device=dev) for _ in range(self.parts - 1)] if dev.type == "cuda" else []
 
     def evaluate(self, actor_cross, actor_wait, actor_choice, episodes=1, choix=False):
         """Deterministic evaluation (Env_rollout.iterations :152-252): `episodes` consecutive
@@ -130,10 +152,15 @@ class RolloutGPU:
                                             self.eps[0].numel(), st))
 
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
-                eps_tape=None, step_events=None):
+                eps_tape=None, step_events=None, parts=None):
         """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
-        replay recorded draws (parity mode); otherwise Philox noise is drawn."""
+        replay recorded draws (parity mode); otherwise Philox noise is drawn.  parts: 1 forces the
+        one-chain loop for this call (default: self.parts); step_events implies it."""
         L = _lib.lib()
+        nparts = self.parts if parts is None else min(int(parts), self.parts)
+        if step_events is not None:
+            nparts = 1
+        self._bufs.parts = nparts
         if forced_choice is None or eps_tape is None:
             self.draw_noise(seed, iteration)
         if eps_tape is not None:
@@ -144,20 +171,43 @@ class RolloutGPU:
         mc, tc = actor_choice.mlp_desc()
         mx, tx = actor_cross.mlp_desc()
         mw, tw = actor_wait.mlp_desc()
-        st = _lib.stream_ptr(device=self.venv.device)
+        dev = self.venv.device
+        st = _lib.stream_ptr(device=dev)
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
-        for t in range(self.T):
-            if self.P == 1:  # features straight into the step's record (include/mhppo.h)
-                self._bufs.feat_c = self.obs_c[t].data_ptr()
-            _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
-                                              ctypes.byref(self._bufs), st))
-            if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
-                step_events[t][0].record()
-            _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
+        if nparts > 1:
+            # Two-stream rollout: the parts' step chains (policy -> env step -> policy ...) are
+            # independent, so one part's policy MFMA work fills the CUs that another part's
+            # latency-bound env step leaves idle (one wave per SIMD, the launch lasting as long as
+            # its slowest wave).  The same kernels and results as the one-chain loop below.
+            main = torch.cuda.current_stream(dev)
+            forked = torch.cuda.Event()
+            forked.record(main)
+            for side in self._side[:nparts - 1]:
+                side.wait_event(forked)
+            streams = [st] + [side.cuda_stream for side in self._side[:nparts - 1]]
+            for t in range(self.T):
+                if self.P == 1:  # features straight into the step's record (include/mhppo.h)
+                    self._bufs.feat_c = self.obs_c[t].data_ptr()
+                for part, sp in enumerate(streams):
+                    _lib.check(L.mhppo_rollout_policy_part(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                                           ctypes.byref(self._bufs), part, sp))
+                    _lib.check(L.mhppo_rollout_sample_env_part(self.venv.handle, _lib.ptr(self.eps[t]), t,
+                                                               ctypes.byref(self._bufs), part, sp))
+            for side in self._side[:nparts - 1]:
+                main.wait_stream(side)
+        else:
+            for t in range(self.T):
+                if self.P == 1:  # features straight into the step's record (include/mhppo.h)
+                    self._bufs.feat_c = self.obs_c[t].data_ptr()
+                _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
                                                   ctypes.byref(self._bufs), st))
-            if step_events is not None:
-                step_events[t][1].record()
+                if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
+                    step_events[t][0].record()
+                _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
+                                                      ctypes.byref(self._bufs), st))
+                if step_events is not None:
+                    step_events[t][1].record()
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
         # obs_c/act/logp/rew: [N, S, T(, 13)] views of the time-major buffers (*_tm)
         return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,

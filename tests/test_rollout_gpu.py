@@ -156,3 +156,29 @@ def test_kernel_timing_events_leave_results_unchanged():
         assert np.array_equal(outs[0][k], outs[1][k]), k
     ms, n = times[0]
     assert n == 50 and ms > 0.0
+
+
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2, 4096), ("scalable", 8, 1, 4, 4000), ("coop", 4, 2, 2, 1000)])
+def test_two_part_rollout_equals_one_chain(case):
+    """RolloutGPU(parts=2): the two env parts' step chains on two streams (mhppo_rollout_policy_part /
+    _sample_env_part, part bounds from k_part_bounds) give bit-identical records to the one-chain
+    loop — including a ragged N (a part boundary at a multiple of 64 envs) and P = 2 pedestrians."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    v, nc, npd, nl, N = case
+    outs = []
+    for parts in (1, 2):
+        venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=900)
+        ro = RolloutGPU(venv, parts=parts)
+        torch.manual_seed(3)
+        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        ad = Model_PPO(ro.dc, 2, 2).cuda()
+        b = ro.collect(ac, aw, ad, seed=2, iteration=1)
+        torch.cuda.synchronize()
+        outs.append({k: getattr(b, k).clone() for k in ("a_d", "closest", "exist", "obs_c", "act", "logp", "rew",
+                                                         "ep_min", "feat_d", "logp_d")})
+        outs[-1]["state"] = venv.state_dict()["blob"]
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
