@@ -757,12 +757,7 @@ constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
 using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
 // per-wave slot: the tile image (also the f32 transpose image), two input slots (double
 // buffered), a second tile image
-#ifndef MHPPO_X3_PF_DEPTH
-#define MHPPO_X3_PF_DEPTH 1
-#endif
-constexpr int PF_DEPTH = MHPPO_X3_PF_DEPTH;  // tiles whose inputs are in flight ahead of the current one
-constexpr int NSLOT = PF_DEPTH + 1;
-constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + NSLOT * LY::IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
+constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
 constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -1424,32 +1419,26 @@ __device__ __forceinline__ void adv_norm(const double *stats, double m_global, f
   stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
 }
 
-// Inputs of this wave's tiles: LDS-DMA PF_DEPTH tiles ahead into a ring of PF_DEPTH + 1 slots;
-// the ragged last tile loads synchronously.  body(slot, row0, nrows) runs each tile.
+// Inputs of this wave's tiles: LDS-DMA one tile ahead into the double-buffered slot; the ragged
+// last tile loads synchronously.  body(slot, row0, nrows) runs each tile.  (Two tiles ahead in a
+// three-slot ring measured no faster: 1.764 / 1.867-1.871 ms vs 1.749-1.776 / 1.869-1.871 ms per
+// critic / actor launch, profiles/r04_x3_probe/ab_pf2.txt.)
 template <int KIND, class Body>
 __device__ __forceinline__ void tile_loop(const WaveSlot &ws, int64_t gw, int64_t nw, int64_t M, const float *X,
                                           const float *ret, const float *V, const float *act, const float *lp_old,
                                           Body &&body) {
   const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
-  constexpr int OPS = prefetch_ops<KIND>();
   int cb = 0;
   MHPPO_MARK(0);
-#pragma unroll
-  for (int k = 0; k < PF_DEPTH; k++)
-    if (gw + k * nw < nfull) prefetch_tile<KIND, LY>(ws.inb + k * LY::IN_SZ, X, ret, V, act, lp_old, (gw + k * nw) * 32, ws.l);
-  for (int64_t tile = gw; tile < ntiles; tile += nw, cb = (cb == NSLOT - 1) ? 0 : cb + 1) {
+  if (gw < nfull) prefetch_tile<KIND, LY>(ws.inb, X, ret, V, act, lp_old, gw * 32, ws.l);
+  for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
     float *slot = ws.inb + cb * LY::IN_SZ;
-    const int64_t ahead = tile + PF_DEPTH * nw;
-    // in vmcnt's issue order, this tile's DMA precedes every later prefetch (and any store):
-    // allowing (tiles still ahead) x OPS outstanding waits for this one
-    if (ahead < nfull) {
-      const int sl = cb + PF_DEPTH >= NSLOT ? cb + PF_DEPTH - NSLOT : cb + PF_DEPTH;
-      prefetch_tile<KIND, LY>(ws.inb + sl * LY::IN_SZ, X, ret, V, act, lp_old, ahead * 32, ws.l);
-      wait_vmcnt<PF_DEPTH * OPS>();
-    } else if (PF_DEPTH > 1 && tile + nw < nfull) {
-      wait_vmcnt<(PF_DEPTH > 1 ? PF_DEPTH - 1 : 0) * OPS>();  // the tiles after this one stay in flight
+    const int64_t nxt = tile + nw;
+    if (nxt < nfull) {
+      prefetch_tile<KIND, LY>(ws.inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, ws.l);
+      wait_vmcnt<prefetch_ops<KIND>()>();
     } else if (tile < nfull) {
       wait_vmcnt<0>();
     } else {
