@@ -744,26 +744,48 @@ struct F3 {  // one MFMA operand fragment (8 elements) as its three bf16 parts
   u32x4 p[3];
 };
 
-constexpr int NIN = NIN_CONT;
 // row strides (bytes) of the bf16 images: odd multiples of 8 B over the data width
-constexpr int W1_ROWB = 40, W2_ROWB = 72, W3_ROWB = 136, IM_ROWB = 72;
-constexpr int W1_PART = 32 * W1_ROWB, W2_PART = 64 * W2_ROWB, W3_PART = 32 * W3_ROWB, IM_PART = 32 * IM_ROWB;
+constexpr int W2_ROWB = 72, W3_ROWB = 136, IM_ROWB = 72;
+constexpr int W2_PART = 64 * W2_ROWB, W3_PART = 32 * W3_ROWB, IM_PART = 32 * IM_ROWB;
 constexpr int IMG = 3 * IM_PART;    // one tile image (three parts) = the per-wave LDS slot
 constexpr int TS = 36;              // f32 transpose image row stride (floats; 16-B aligned rows)
 static_assert(32 * TS * 4 <= IMG, "the f32 image shares the slot");
-constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_F = O_W3 + 3 * W3_PART;
-constexpr int NF = 64 + 32 + 32 + 4;  // f32 params: b2[64] b3[32] w4[32] b4
-constexpr int O_WAVE = (O_F + NF * 4 + 15) / 16 * 16;
-using LY = Lay<7, true, 1>;         // input-slot geometry of the f32 path (X 32x13 | ret V | act logp)
-// per-wave slot: the tile image (also the f32 transpose image), two input slots (double
-// buffered), a second tile image
-constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * LY::IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
 constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
-constexpr int LDS_BYTES = O_WAVE + WAVES * WAVE_B;
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-constexpr int LDS_BYTES_PAIR = 2 * O_WAVE + WAVES * WAVE_B;  // two nets' weights (k_mlp_train_x3_pair)
-static_assert(LDS_BYTES_PAIR <= 160 * 1024, "LDS budget (pair)");
-static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0, "16-B aligned slots");
+
+// Geometry of one split-precision net: K1 = layer-1 K (the inputs and the bias column, padded to
+// whole 16-deep K-steps), NOUT outputs, NIC the compile-time input count (0: a kernel argument,
+// nin <= K1 - 1).  LDS: the net's weights (bf16 images of W1..W3, f32 b2 b3 w4 b4), then per
+// wave: the tile image (also the f32 transpose image), two input slots (double buffered), a
+// second tile image.
+template <int K1_, int NOUT_, int NIC_>
+struct Geo {
+  static constexpr int K1 = K1_, KS1 = K1 / 16, NOUT = NOUT_, NIC = NIC_;
+  static_assert(K1 % 16 == 0 && (NIC == 0 || NIC < K1), "layer-1 geometry");
+  static constexpr int W1_ROWB = 2 * K1 + 8, W1_PART = 32 * W1_ROWB;
+  static constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_F = O_W3 + 3 * W3_PART;
+  static constexpr int F_W4 = 96, F_B4 = F_W4 + 32 * NOUT, NF = F_B4 + NOUT;  // f32: b2[64] b3[32] w4 b4
+  static constexpr int NET_B = (O_F + NF * 4 + 15) / 16 * 16;
+  // input slot (floats): X [32][nin] | s0 [32 | 32] | s1 [32 | 32].  A runtime nin gets an X region
+  // of whole 1-KiB pieces, so every LDS-DMA piece lands unmasked (zeros past the rows).
+  static constexpr int XMAX = NIC ? (32 * NIC + 3) / 4 * 4 : (32 * (K1 - 1) + 255) / 256 * 256;
+  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = XMAX + 64, IN_SZ = XMAX + 128;
+  static constexpr int XPIECES = (XMAX * 4 + 1023) / 1024;
+  static constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
+  static constexpr int LDS_BYTES = NET_B + WAVES * WAVE_B;
+  static constexpr int LDS_BYTES_PAIR = 2 * NET_B + WAVES * WAVE_B;  // two nets' weights (pair kernel)
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(WAVE_B % 16 == 0 && O_IN % 16 == 0 && IN_SZ % 4 == 0, "16-B aligned slots");
+};
+// the 13-input continuous heads (the big batches): the slot layout of the f32 path's Lay<7, true, 1>
+using G13 = Geo<16, 1, NIN_CONT>;
+using LY = Lay<7, true, 1>;
+static_assert(G13::IN_S0 == LY::IN_S0 && G13::IN_S1 == LY::IN_S1 && G13::IN_SZ == LY::IN_SZ, "13-input slot");
+static_assert(G13::LDS_BYTES_PAIR <= 160 * 1024, "LDS budget (pair)");
+// the choice heads' nets on this kernel: up to 31 inputs (wider ones stay on the f32 kernel)
+using GC16 = Geo<16, 2, 0>;
+using GV16 = Geo<16, 1, 0>;
+using GC32 = Geo<32, 2, 0>;
+using GV32 = Geo<32, 1, 0>;
 
 #ifdef MHPPO_X3_PHASE
 __device__ __forceinline__ void x3_phase() { __builtin_amdgcn_sched_barrier(0); }
@@ -892,6 +914,11 @@ __device__ __forceinline__ void macc6_16_w(const F3 &a, const F3 &b, f32x4 &c) {
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
 }
+__device__ __forceinline__ void macc_drain2(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f,
+                                            f32x4 &g, f32x4 &h) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f), "+a"(g),
+               "+a"(h));
+}
 __device__ __forceinline__ uint2 lds_u2(const char *p) { return *reinterpret_cast<const uint2 *>(p); }
 __device__ __forceinline__ uint2 tr16(const char *p) {
   v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16 *)(p));
@@ -999,44 +1026,55 @@ __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 // step (spills), a software-pipelined loop (backward of tile i beside the forward of tile i+1:
 // 10 % slower).
 namespace x3 {
-constexpr int G_W1 = 0, G_B1 = 32 * NIN, G_W2 = G_B1 + 32, G_B2 = G_W2 + 64 * 32, G_W3 = G_B2 + 64,
-              G_B3 = G_W3 + 32 * 64, G_W4 = G_B3 + 32, G_B4 = G_W4 + 32, NWP = G_B4 + 1;
-constexpr int NET_B = O_WAVE;  // LDS bytes of one net's staged weights (bf16 images + f32 params)
+// packed torch-layout offsets of one Model_PPO (W1 b1 W2 b2 W3 b3 W4 b4)
+struct Packed {
+  int W1, B1, W2, B2, W3, B3, W4, B4, NP;
+  __host__ __device__ constexpr Packed(int nin, int nout)
+      : W1(0), B1(32 * nin), W2(B1 + 32), B2(W2 + 64 * 32), W3(B2 + 64), B3(W3 + 32 * 64), W4(B3 + 32),
+        B4(W4 + 32 * nout), NP(B4 + nout) {}
+};
+template <class G>
+__device__ __forceinline__ int geo_nin(int nin_rt) { return G::NIC ? G::NIC : nin_rt; }
 
-// Stage one net's weights at Lw: bf16 images (three parts), b1 as input column 13 of W1.  Every
+// Stage one net's weights at Lw: bf16 images (three parts), b1 as input column nin of W1.  Every
 // global load is issued before the first LDS store (one memory round trip per launch; a strided
 // load -> split -> store loop per array costs one dependent trip per iteration).
-__device__ __forceinline__ void stage_net(const float *__restrict__ W, char *Lw, int tid) {
-  constexpr int nin = NIN;
-  float *F = reinterpret_cast<float *>(Lw + O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, 128) b4 [128]
-  constexpr int NT = 64 * WAVES, N1 = (32 * 16 + NT - 1) / NT, N2 = 2048 / NT, NFQ = (NF + NT - 1) / NT;
+template <class G>
+__device__ __forceinline__ void stage_net(const float *__restrict__ W, char *Lw, int tid, int nin_rt) {
+  const int nin = geo_nin<G>(nin_rt);
+  const Packed P(nin, G::NOUT);
+  constexpr int K1 = G::K1, NF = G::NF;
+  float *F = reinterpret_cast<float *>(Lw + G::O_F);  // b2 [0, 64) b3 [64, 96) w4 [96, ...) b4
+  constexpr int NT = 64 * WAVES, N1 = (32 * K1 + NT - 1) / NT, N2 = 2048 / NT, NFQ = (NF + NT - 1) / NT;
   static_assert(2048 % NT == 0, "staging: block size");
   float v1[N1], v2[N2], v3[N2], vf[NFQ];
 #pragma unroll
   for (int q = 0; q < N1; q++) {
-    const int i = tid + q * NT, r = i >> 4, c = i & 15;
-    v1[q] = i >= 32 * 16 ? 0.0f : (c < nin ? W[G_W1 + r * nin + c] : (c == nin ? W[G_B1 + r] : 0.0f));
+    const int i = tid + q * NT, r = i / K1, c = i % K1;
+    v1[q] = i >= 32 * K1 ? 0.0f : (c < nin ? W[P.W1 + r * nin + c] : (c == nin ? W[P.B1 + r] : 0.0f));
   }
 #pragma unroll
   for (int q = 0; q < N2; q++) {
-    v2[q] = W[G_W2 + tid + q * NT];
-    v3[q] = W[G_W3 + tid + q * NT];
+    v2[q] = W[P.W2 + tid + q * NT];
+    v3[q] = W[P.W3 + tid + q * NT];
   }
 #pragma unroll
   for (int q = 0; q < NFQ; q++) {
     const int i = tid + q * NT;
-    vf[q] = i < 64 ? W[G_B2 + i] : (i < 96 ? W[G_B3 + i - 64] : (i < 128 ? W[G_W4 + i - 96] : (i == 128 ? W[G_B4] : 0.f)));
+    vf[q] = i < 64 ? W[P.B2 + i]
+                   : (i < 96 ? W[P.B3 + i - 64]
+                             : (i < G::F_B4 ? W[P.W4 + i - 96] : (i < NF ? W[P.B4 + i - G::F_B4] : 0.f)));
   }
 #pragma unroll
   for (int q = 0; q < N1; q++) {
     const int i = tid + q * NT;
-    if (i < 32 * 16) stage_w(Lw + O_W1, W1_PART, W1_ROWB, i >> 4, i & 15, v1[q]);
+    if (i < 32 * K1) stage_w(Lw + G::O_W1, G::W1_PART, G::W1_ROWB, i / K1, i % K1, v1[q]);
   }
 #pragma unroll
   for (int q = 0; q < N2; q++) {
     const int i = tid + q * NT;
-    stage_w(Lw + O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, v2[q]);
-    stage_w(Lw + O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, v3[q]);
+    stage_w(Lw + G::O_W2, W2_PART, W2_ROWB, i >> 5, i & 31, v2[q]);
+    stage_w(Lw + G::O_W3, W3_PART, W3_ROWB, i >> 6, i & 63, v3[q]);
   }
 #pragma unroll
   for (int q = 0; q < NFQ; q++) {
@@ -1046,6 +1084,7 @@ __device__ __forceinline__ void stage_net(const float *__restrict__ W, char *Lw,
 }
 
 // The per-wave lane geometry of the wave's LDS slot (images, f32 transpose image, input slots)
+template <class GEO>
 struct WaveSlot {
   char *wb;          // this wave's image / f32 transpose slot
   float *T;          // f32 transpose image (shares the slot)
@@ -1056,9 +1095,9 @@ struct WaveSlot {
   int l, j, kh, G;
   __device__ __forceinline__ WaveSlot(char *L8, int w, int l_) : l(l_), j(l_ & 31), kh(l_ >> 5), G(l_ >> 4) {
     const int q4 = (l >> 2) & 3, p4 = l & 3;
-    wb = L8 + w * WAVE_B;
+    wb = L8 + w * GEO::WAVE_B;
     T = reinterpret_cast<float *>(wb);
-    inb = reinterpret_cast<float *>(wb + O_IN);
+    inb = reinterpret_cast<float *>(wb + GEO::O_IN);
     imw = wb + j * IM_ROWB + 8 * kh;
     // image reads: rows 8 (G >> 1) + 4u + q, chunk 4 (G & 1) + p
     imr = wb + (8 * (G >> 1) + q4) * IM_ROWB + 8 * (4 * (G & 1) + p4);
@@ -1072,29 +1111,41 @@ struct WaveSlot {
 // held in registers too (one critic pass alone; the actor pass's loss, and a second net in the
 // same wave, need those registers) — and then dW2 cannot carry its image reads in its MFMA gaps.
 // HB: the backward (W^T) fragments are held in registers (not with two nets in one wave).
-template <int KIND, bool HF, bool HB = true>
+// G: the net's geometry (inputs, outputs); K_CHOICE: the choice actor (two outputs, softmax pair).
+template <int KIND, bool HF, bool HB, class G>
 struct Pass {
+  static constexpr int KS1 = G::KS1, NOUT = G::NOUT;
+  static_assert(NOUT == (KIND == K_CHOICE ? 2 : 1), "outputs");
   const char *w1row, *w2row, *w3row, *w2tr, *w3tr;
   const float *F;
-  float b40;
+  float b40, b41;
+  int nin;
+  const double *counts;  // K_CHOICE: the global action counts (nullptr: per-row mode)
+  double m_global;
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
   f32x16 gW2a, gW2b, gW3a, gW3b;
-  f32x4 gW1t[2];
-  float gsum[5];  // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4 gB4
+  f32x4 gW1t[KS1][2];
+  // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4[0] gB4[0] gW4[1] gB4[1]
+  float gsum[7];
   // float64 loss / advantage sums in registers (lanes kh == 0), folded once after the loop: an
   // LDS read-modify-write per tile put its latency on the loss section's serial chain (-1 %)
   double dsum0, dsum1, dsum2;
 
-  __device__ __forceinline__ void init(const char *Lw, const WaveSlot &ws) {
-    const int j = ws.j, kh = ws.kh, G = ws.G, q4 = (ws.l >> 2) & 3, p4 = ws.l & 3;
+  __device__ __forceinline__ void init(const char *Lw, const WaveSlot<G> &ws, int nin_rt = 0,
+                                       const double *counts_ = nullptr, double m_global_ = 0.0) {
+    const int j = ws.j, kh = ws.kh, G_ = ws.G, q4 = (ws.l >> 2) & 3, p4 = ws.l & 3;
+    nin = geo_nin<G>(nin_rt);
+    counts = counts_;
+    m_global = m_global_;
     // lane address bases: every fragment access is one of these plus a constant
-    w1row = Lw + O_W1 + j * W1_ROWB + 16 * kh;
-    w2row = Lw + O_W2 + j * W2_ROWB + 8 * kh;
-    w3row = Lw + O_W3 + j * W3_ROWB + 8 * kh;
-    w2tr = Lw + O_W2 + (4 * (G >> 1) + q4) * W2_ROWB + 8 * (4 * (G & 1) + p4);
-    w3tr = Lw + O_W3 + (4 * (G >> 1) + q4) * W3_ROWB + 8 * (4 * (G & 1) + p4);
-    F = reinterpret_cast<const float *>(Lw + O_F);
-    b40 = uniform_f(F[128]);
+    w1row = Lw + G::O_W1 + j * G::W1_ROWB + 16 * kh;
+    w2row = Lw + G::O_W2 + j * W2_ROWB + 8 * kh;
+    w3row = Lw + G::O_W3 + j * W3_ROWB + 8 * kh;
+    w2tr = Lw + G::O_W2 + (4 * (G_ >> 1) + q4) * W2_ROWB + 8 * (4 * (G_ & 1) + p4);
+    w3tr = Lw + G::O_W3 + (4 * (G_ >> 1) + q4) * W3_ROWB + 8 * (4 * (G_ & 1) + p4);
+    F = reinterpret_cast<const float *>(Lw + G::O_F);
+    b40 = uniform_f(F[G::F_B4]);
+    b41 = NOUT == 2 ? uniform_f(F[G::F_B4 + 1]) : 0.0f;
     // loop-invariant weight fragments read from LDS once
     if constexpr (HF) {
       for (int t = 0; t < 2; t++)
@@ -1107,9 +1158,8 @@ struct Pass {
       for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
     }
     gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
-    gW1t[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gW1t[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < 5; k++) gsum[k] = 0.f;
+    for (int c = 0; c < KS1; c++) gW1t[c][0] = gW1t[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 7; k++) gsum[k] = 0.f;
     dsum0 = dsum1 = dsum2 = 0.0;
   }
   __device__ __forceinline__ F3 fw2(int t, int s) const {
@@ -1132,28 +1182,33 @@ struct Pass {
   // One 32-row tile whose inputs sit in `slot` (X [32][13] | ret V | act logp_old).  The critic
   // writes V (rows row0 .. row0 + nrows) to Vout; the actor normalises A = ret - V with
   // (meanf, stdf).
-  __device__ __forceinline__ void tile(const WaveSlot &ws, const float *slot, int64_t row0, int nrows,
+  __device__ __forceinline__ void tile(const WaveSlot<G> &ws, const float *slot, int64_t row0, int nrows,
                                        float *__restrict__ Vout, float meanf, float stdf, double inv_m,
                                        float out_mean, float out_std) {
-    constexpr int nin = NIN;
-    const int l = ws.l, j = ws.j, kh = ws.kh, G = ws.G;
+    const int nin = G::NIC ? G::NIC : this->nin;
+    const int l = ws.l, j = ws.j, kh = ws.kh, G_ = ws.G;
     float *T = ws.T;
     char *imw = ws.imw;
     const char *imr = ws.imr, *imr16 = ws.imr16;
+    constexpr int O_IM2 = G::O_IM2;
     auto radd = [&](int k, float v) { gsum[k] += v; };
-    const float *Xs = slot + LY::IN_X;
-    // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column 13)
+    const float *Xs = slot + G::IN_X;
+    // ---- layer 1: h1^T = W1 . [X | 1]^T (b1 rides in input column nin), K-step s = columns 16s..
     auto layer1 = [&]() {
-      float v8[8];
+      f32x16 h = zero16();
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        // row j, input column k = 8h + q (h = 1: columns 8..15; 13 is the bias input).  Columns
-        // 13-15 read the next row's first inputs (the slot's last row reads into its s0 block).
-        const int k = 8 * kh + q;
-        const float v = Xs[j * nin + 8 * kh + q];
-        v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
+      for (int s = 0; s < KS1; s++) {
+        float v8[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          // row j, input column k = 16s + 8h + q (the bias input at k = nin).  Columns past nin
+          // read the next row's first inputs (the slot's last row reads into its s0 block).
+          const int k = 16 * s + 8 * kh + q;
+          const float v = Xs[j * nin + k];
+          v8[q] = k < nin ? v : (k == nin ? 1.0f : 0.0f);
+        }
+        h = mfma6(rd_pair<G::W1_PART>(w1row + 32 * s, 8), split8(v8), h);
       }
-      f32x16 h = mfma6(rd_pair<W1_PART>(w1row, 8), split8(v8), zero16());
       relu16(h);
       return h;
     };
@@ -1182,15 +1237,24 @@ struct Pass {
     x3_phase();
     MHPPO_MARK(4);
     // ---- output and loss gradient dL/dy for this lane's row (as the f32 path)
-    const f32x16 w4v = feat_vec(F + 96, kh);
+    const f32x16 w4v = feat_vec(F + G::F_W4, kh);
     float part0 = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; r++) part0 = fmaf(w4v[r], h3[r], part0);
     const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
+    f32x16 w4v1;
+    float y1 = 0.0f;
+    if constexpr (NOUT == 2) {
+      w4v1 = feat_vec(F + G::F_W4 + 32, kh);
+      float part1 = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) part1 = fmaf(w4v1[r], h3[r], part1);
+      y1 = (part1 + __shfl_xor(part1, 32)) + b41;
+    }
     const bool valid = j < nrows;
-    float dy0 = 0.0f;
+    float dy0 = 0.0f, dy1 = 0.0f;
     if (valid) {
-      const float rt = slot[LY::IN_S0 + j];
+      const float rt = slot[G::IN_S0 + j];
       if constexpr (KIND == K_CRITIC) {
         const float v = y0;
         if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 128), 4 * j, 0, 0);
@@ -1202,34 +1266,80 @@ struct Pass {
           dsum2 += (double)a * (double)a;
         }
         dy0 = (float)(2.0 * inv_m * (double)d);
-      } else {
+      } else if constexpr (KIND == K_CONT) {
         const float t = tanhf(y0);
         const float mu = t * out_std + out_mean;
-        const float a = rt - slot[LY::IN_S0 + 32 + j];
+        const float a = rt - slot[G::IN_S0 + 32 + j];
         const float A = (a - meanf) / (stdf + 1e-10f);
-        const float diff = (float)((double)slot[LY::IN_S1 + j] - (double)mu);
+        const float diff = (float)((double)slot[G::IN_S1 + j] - (double)mu);
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-        const double r = exp((double)lp - (double)slot[LY::IN_S1 + 32 + j]);
+        const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
         double dfdr;
         const double f = surr_and_grad(r, (double)A, dfdr);
         if (kh == 0) dsum0 += f;
         const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
         dy0 = (dmu * out_std) * (1.0f - t * t);
+      } else {
+        // choice actor (train_model_d :818-851): softmax over the pair (as torch: shift by the
+        // max), pn = p / (p0 + p1), the M x M Categorical broadcast in its O(M) form with the
+        // global action counts (or the opt-in per-row loss: the row's own action, weight M)
+        const float mx = fmaxf(y0, y1);
+        const float e0 = expf(y0 - mx), e1 = expf(y1 - mx);
+        const float se = e0 + e1;
+        const float p[2] = {e0 / se, e1 / se};
+        const float a = rt - slot[G::IN_S0 + 32 + j];
+        const float A = (a - meanf) / (stdf + 1e-10f);
+        const double old = (double)slot[G::IN_S1 + j];
+        const float sp = p[0] + p[1];
+        const float pn[2] = {p[0] / sp, p[1] / sp};
+        const float eps = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
+        const double inv_m2 = inv_m * inv_m;
+        const int a_row = counts ? 0 : (int)slot[G::IN_S1 + 32 + j];
+        double dlp[2], f = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const double wk = counts ? counts[k] : (k == a_row ? m_global : 0.0);
+          const float pc = pn[k] < eps ? eps : (pn[k] > hi ? hi : pn[k]);
+          const double r = exp((double)logf(pc) - old);
+          double dfdr;
+          const double fk = surr_and_grad(r, (double)A, dfdr);
+          if (wk != 0.0) f += wk * fk;
+          const double pass = (pn[k] >= eps && pn[k] <= hi) ? 1.0 : 0.0;
+          dlp[k] = inv_m2 * wk * dfdr * r * pass / (double)pc;  // dL/dpn_k
+        }
+        if (kh == 0) dsum0 += f;
+        const double sd = (double)sp;
+        const double g0 = (dlp[0] * (1.0 - pn[0]) - dlp[1] * pn[1]) / sd;  // dL/dp_k
+        const double g1 = (dlp[1] * (1.0 - pn[1]) - dlp[0] * pn[0]) / sd;
+        const double dot = (double)p[0] * g0 + (double)p[1] * g1;
+        dy0 = (float)((double)p[0] * (g0 - dot));  // softmax Jacobian
+        dy1 = (float)((double)p[1] * (g1 - dot));
       }
     }
     radd(4, (kh == 0) ? dy0 : 0.0f);
+    if constexpr (NOUT == 2) radd(6, (kh == 0) ? dy1 : 0.0f);
     // ---- layer 4 backward: d3 = dH3^T masked; dW4 = row sums of dy h3; dB3 = row sums of d3
     f32x16 g, d3;
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       g[r] = dy0 * h3[r];
-      d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
+      if constexpr (NOUT == 2) d3[r] = (h3[r] > 0.0f) ? fmaf(w4v1[r], dy1, w4v[r] * dy0) : 0.0f;
+      else d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
     }
     put_t(T, g, l);
     lds_order();
     radd(3, half_row_sum(T, l));
     lds_order();
+    if constexpr (NOUT == 2) {
+      f32x16 g1;
+#pragma unroll
+      for (int r = 0; r < 16; r++) g1[r] = dy1 * h3[r];
+      put_t(T, g1, l);
+      lds_order();
+      radd(5, half_row_sum(T, l));
+      lds_order();
+    }
     put_t(T, d3, l);
     lds_order();
     radd(2, half_row_sum(T, l));
@@ -1340,17 +1450,28 @@ struct Pass {
     img_write(imw, split_step(d1, 0), split_step(d1, 1));
     lds_order();
     {
-      float xv[8];
-      const int n = l & 15;
+      // the B operand of input columns 16c .. 16c + 15: rows 8G .. 8G + 7 of column 16c + n
+      auto xcols = [&](int c) {
+        float xv[8];
+        const int n = 16 * c + (l & 15);
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const float v = Xs[(8 * G + q) * nin + (n < nin ? n : 0)];
-        xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
-      }
-      const F3 b = split8(xv);
+        for (int q = 0; q < 8; q++) {
+          const float v = Xs[(8 * G_ + q) * nin + (n < nin ? n : 0)];
+          xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
+        }
+        return split8(xv);
+      };
+      const F3 b = xcols(0);
+      const F3 a0 = tr_pair<IM_PART>(imr16, 4 * IM_ROWB);
       F3 a1;
-      macc6_16_rd<false, 32>(tr_pair<IM_PART>(imr16, 4 * IM_ROWB), b, gW1t[0], a1, imr16);
-      macc6_16_w(a1, b, gW1t[1]);
+      macc6_16_rd<false, 32>(a0, b, gW1t[0][0], a1, imr16);
+      macc6_16_w(a1, b, gW1t[0][1]);
+#pragma unroll
+      for (int c = 1; c < KS1; c++) {
+        const F3 bc = xcols(c);
+        macc6_16(a0, bc, gW1t[c][0]);
+        macc6_16(a1, bc, gW1t[c][1]);
+      }
     }
     lds_order();
     x3_phase();
@@ -1358,26 +1479,32 @@ struct Pass {
   }
 
   // this wave's partial gradient (packed torch layout) and float64 sums
-  __device__ __forceinline__ void finish(const WaveSlot &ws, float *__restrict__ gp, double *__restrict__ dp) {
-    constexpr int nin = NIN;
-    const int l = ws.l, j = ws.j, kh = ws.kh, G = ws.G;
-    macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0], gW1t[1]);
+  __device__ __forceinline__ void finish(const WaveSlot<G> &ws, float *__restrict__ gp, double *__restrict__ dp) {
+    const int nin = G::NIC ? G::NIC : this->nin;
+    const Packed P(nin, NOUT);
+    const int l = ws.l, j = ws.j, kh = ws.kh, G_ = ws.G;
+    if constexpr (KS1 == 1) macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0][0], gW1t[0][1]);
+    else macc_drain2(gW2a, gW2b, gW3a, gW3b, gW1t[0][0], gW1t[0][1], gW1t[KS1 - 1][0], gW1t[KS1 - 1][1]);
     float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
+    float gW41 = gsum[5], gB41 = gsum[6];
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int f = feat(r, l);
-      gp[G_W2 + f * 32 + j] = gW2a[r];
-      gp[G_W2 + (32 + f) * 32 + j] = gW2b[r];
-      gp[G_W3 + f * 64 + j] = gW3a[r];
-      gp[G_W3 + f * 64 + 32 + j] = gW3b[r];
+      gp[P.W2 + f * 32 + j] = gW2a[r];
+      gp[P.W2 + (32 + f) * 32 + j] = gW2b[r];
+      gp[P.W3 + f * 64 + j] = gW3a[r];
+      gp[P.W3 + f * 64 + 32 + j] = gW3b[r];
     }
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int c = 0; c < KS1; c++) {
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int f = 16 * t + 4 * G + r, n = l & 15;
-        if (n < nin) gp[G_W1 + f * nin + n] = gW1t[t][r];
-        if (n == nin) gp[G_B1 + f] = gW1t[t][r];
+      for (int t = 0; t < 2; t++) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int f = 16 * t + 4 * G_ + r, n = 16 * c + (l & 15);
+          if (n < nin) gp[P.W1 + f * nin + n] = gW1t[c][t][r];
+          if (n == nin) gp[P.B1 + f] = gW1t[c][t][r];
+        }
       }
     }
     // halves of the row sums: lanes j and j + 32 hold rows 0-15 / 16-31 of feature j
@@ -1385,15 +1512,20 @@ struct Pass {
     gB2b += __shfl_xor(gB2b, 32);
     gB3 += __shfl_xor(gB3, 32);
     gW4 += __shfl_xor(gW4, 32);
+    if (NOUT == 2) gW41 += __shfl_xor(gW41, 32);
     if (kh == 0) {
-      gp[G_B2 + j] = gB2a;
-      gp[G_B2 + 32 + j] = gB2b;
-      gp[G_B3 + j] = gB3;
-      gp[G_W4 + j] = gW4;
+      gp[P.B2 + j] = gB2a;
+      gp[P.B2 + 32 + j] = gB2b;
+      gp[P.B3 + j] = gB3;
+      gp[P.W4 + j] = gW4;
+      if (NOUT == 2) gp[P.W4 + 32 + j] = gW41;
     }
-    float b4s0 = gB4;
+    float b4s0 = gB4, b4s1 = gB41;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) b4s0 += __shfl_xor(b4s0, o);
+    for (int o = 32; o > 0; o >>= 1) {
+      b4s0 += __shfl_xor(b4s0, o);
+      if (NOUT == 2) b4s1 += __shfl_xor(b4s1, o);
+    }
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     if (kh == 0) s0 = dsum0, s1 = dsum1, s2 = dsum2;
 #pragma unroll
@@ -1403,7 +1535,8 @@ struct Pass {
       s2 += __shfl_xor(s2, o);
     }
     if (l == 0) {
-      gp[G_B4] = b4s0;
+      gp[P.B4] = b4s0;
+      if (NOUT == 2) gp[P.B4 + 1] = b4s1;
       dp[0] = s0;
       dp[1] = s1;
       dp[2] = s2;
@@ -1419,30 +1552,77 @@ __device__ __forceinline__ void adv_norm(const double *stats, double m_global, f
   stdf = uniform_f((float)sqrt(var > 0 ? var : 0.0));
 }
 
+// Tile inputs of a runtime-width geometry (the choice heads): the X rows as whole 1-KiB LDS-DMA
+// pieces (unmasked: buffer loads past the tile's rows return zeros, which land inside the X
+// region), s0 = [ret | V], s1 = [logp_old | action] (K_CHOICE; the action only in per-row mode,
+// else the lanes re-read logp_old: the same instruction count either way).
+template <int KIND, class G>
+__device__ __forceinline__ void prefetch_g(float *slot, const float *X, int nin, const float *ret, const float *V,
+                                           const float *act, const float *lp, int64_t row0, int l) {
+  const v4i rx = rsrc_v(X + row0 * nin, 32 * nin * 4);
+#pragma unroll
+  for (int c = 0; c < G::XPIECES; c++) dma16(rx, slot + G::IN_X + 256 * c, 1024 * c + 16 * l);
+  const uint32_t vo = 4 * (l & 31);
+  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + G::IN_S0, vo);
+  if (KIND != K_CRITIC) {
+    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + G::IN_S0, vo);
+    if (l < 32) dma4(rsrc_v(lp + row0, 128), slot + G::IN_S1, vo);
+    if (l >= 32) dma4(rsrc_v((act ? act : lp) + row0, 128), slot + G::IN_S1, vo);
+  }
+}
+template <int KIND, class G>
+constexpr int prefetch_g_ops() { return G::XPIECES + (KIND == K_CRITIC ? 1 : 4); }
+
+template <int KIND, class G>
+__device__ __forceinline__ void load_sync_g(float *slot, const float *X, int nin, const float *ret, const float *V,
+                                            const float *act, const float *lp, int64_t row0, int nrows, int l) {
+  constexpr int NX = G::XMAX / 64;
+  static_assert(G::XMAX % 64 == 0, "X region");
+  const auto rx = rsrc(X + row0 * nin, (uint32_t)(nrows * nin) * 4);
+  float x[NX];
+#pragma unroll
+  for (int i = 0; i < NX; i++) x[i] = bload(rx, 4 * (l + 64 * i));  // past the rows: 0
+  const uint32_t nb = 4 * nrows, vo = 4 * (l & 31);
+  const float s0 = bload(rsrc((l < 32 || KIND == K_CRITIC) ? ret + row0 : V + row0, nb), vo);
+  float s1 = 0.0f;
+  if (KIND != K_CRITIC) s1 = bload(rsrc((l < 32 || act == nullptr) ? lp + row0 : act + row0, nb), vo);
+#pragma unroll
+  for (int i = 0; i < NX; i++) slot[G::IN_X + l + 64 * i] = x[i];
+  slot[G::IN_S0 + l] = s0;
+  slot[G::IN_S1 + l] = s1;
+}
+
 // Inputs of this wave's tiles: LDS-DMA one tile ahead into the double-buffered slot; the ragged
 // last tile loads synchronously.  body(slot, row0, nrows) runs each tile.  (Two tiles ahead in a
 // three-slot ring measured no faster: 1.764 / 1.867-1.871 ms vs 1.749-1.776 / 1.869-1.871 ms per
 // critic / actor launch, profiles/r04_x3_probe/ab_pf2.txt.)
-template <int KIND, class Body>
-__device__ __forceinline__ void tile_loop(const WaveSlot &ws, int64_t gw, int64_t nw, int64_t M, const float *X,
-                                          const float *ret, const float *V, const float *act, const float *lp_old,
-                                          Body &&body) {
+template <int KIND, class G, class Body>
+__device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int64_t nw, int64_t M, const float *X,
+                                          int nin, const float *ret, const float *V, const float *act,
+                                          const float *lp_old, Body &&body) {
   const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
+  constexpr bool FIXED = G::NIC == NIN_CONT;  // the 13-input heads: the f32 path's slot loaders
+  auto prefetch = [&](float *slot, int64_t row0) {
+    if constexpr (FIXED) prefetch_tile<KIND, LY>(slot, X, ret, V, act, lp_old, row0, ws.l);
+    else prefetch_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, ws.l);
+  };
   int cb = 0;
   MHPPO_MARK(0);
-  if (gw < nfull) prefetch_tile<KIND, LY>(ws.inb, X, ret, V, act, lp_old, gw * 32, ws.l);
+  if (gw < nfull) prefetch(ws.inb, gw * 32);
   for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
-    float *slot = ws.inb + cb * LY::IN_SZ;
+    float *slot = ws.inb + cb * G::IN_SZ;
     const int64_t nxt = tile + nw;
     if (nxt < nfull) {
-      prefetch_tile<KIND, LY>(ws.inb + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, ws.l);
-      wait_vmcnt<prefetch_ops<KIND>()>();
+      prefetch(ws.inb + (cb ^ 1) * G::IN_SZ, nxt * 32);
+      if constexpr (FIXED) wait_vmcnt<prefetch_ops<KIND>()>();
+      else wait_vmcnt<prefetch_g_ops<KIND, G>()>();
     } else if (tile < nfull) {
       wait_vmcnt<0>();
     } else {
-      load_tile_sync<KIND, LY>(slot, X, NIN, ret, V, act, lp_old, row0, nrows, ws.l);
+      if constexpr (FIXED) load_tile_sync<KIND, LY>(slot, X, NIN_CONT, ret, V, act, lp_old, row0, nrows, ws.l);
+      else load_sync_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, nrows, ws.l);
     }
     wave_sync();  // the tile's inputs have landed
     MHPPO_MARK(1);  // timing builds: the tile-input wait
@@ -1452,31 +1632,33 @@ __device__ __forceinline__ void tile_loop(const WaveSlot &ws, int64_t gw, int64_
 }
 }  // namespace x3
 
-template <int KIND>
+template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
-    k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int64_t M, const float *__restrict__ ret,
-                   float *__restrict__ V, const float *__restrict__ act, const float *__restrict__ lp_old,
-                   const double *__restrict__ stats, double m_global, float out_mean, float out_std,
+    k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
+                   const float *__restrict__ ret, float *__restrict__ V, const float *__restrict__ act,
+                   const float *__restrict__ lp_old, const double *__restrict__ stats,
+                   const double *__restrict__ counts, double m_global, float out_mean, float out_std,
                    float *__restrict__ gpart, double *__restrict__ dpart) {
   using namespace x3;
   extern __shared__ float lds[];
   char *L8 = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  stage_net(W, L8, tid);
+  stage_net<G>(W, L8, tid, nin);
   __syncthreads();
-  const WaveSlot ws(L8 + NET_B, w, l);
-  // the critic pass alone holds its forward weight fragments in registers
-  Pass<KIND, KIND == K_CRITIC> p;
-  p.init(L8, ws);
+  const WaveSlot<G> ws(L8 + G::NET_B, w, l);
+  // the 13-input critic pass alone holds its forward weight fragments in registers (with a
+  // runtime input count the choice critic has no registers for them: 23-38 spills)
+  Pass<KIND, KIND == K_CRITIC && G::NIC == NIN_CONT, true, G> p;
+  p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
   if (KIND != K_CRITIC) adv_norm(stats, m_global, meanf, stdf);
   const double inv_m = uniform_d(1.0 / m_global);
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  tile_loop<KIND>(ws, gw, nw, M, X, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
+  tile_loop<KIND, G>(ws, gw, nw, M, X, nin, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
     p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
   });
-  p.finish(ws, gpart + (size_t)gw * NWP, dpart + gw * 3);
+  p.finish(ws, gpart + (size_t)gw * Packed(geo_nin<G>(nin), G::NOUT).NP, dpart + gw * 3);
 }
 
 // Actor pass of epoch e fused with the critic pass of epoch e + 1 (Algo_PPO.train_model_c
@@ -1501,22 +1683,24 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   char *L8 = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  stage_net(Wa, L8, tid);
-  stage_net(Wc, L8 + NET_B, tid);
+  using G = G13;
+  stage_net<G>(Wa, L8, tid, NIN_CONT);
+  stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
-  const WaveSlot ws(L8 + 2 * NET_B, w, l);
-  Pass<K_CONT, false, PAIR_HB> pa;
-  Pass<K_CRITIC, false, PAIR_HB> pc;
+  const WaveSlot<G> ws(L8 + 2 * G::NET_B, w, l);
+  Pass<K_CONT, false, PAIR_HB, G> pa;
+  Pass<K_CRITIC, false, PAIR_HB, G> pc;
   pa.init(L8, ws);
-  pc.init(L8 + NET_B, ws);
+  pc.init(L8 + G::NET_B, ws);
   float meanf, stdf;
   adv_norm(stats, m_global, meanf, stdf);
   const double inv_m = uniform_d(1.0 / m_global);
   const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  tile_loop<K_CONT>(ws, gw, nw, M, X, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
+  tile_loop<K_CONT, G>(ws, gw, nw, M, X, NIN_CONT, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
     pa.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
     pc.tile(ws, slot, row0, nrows, V, 0.f, 1.f, inv_m, out_mean, out_std);
   });
+  constexpr int NWP = Packed(NIN_CONT, 1).NP;
   pa.finish(ws, gpart + (size_t)gw * NWP, dpart + gw * 3);
   pc.finish(ws, gpart + (size_t)(nw + gw) * NWP, dpart + (nw + gw) * 3);
 }
@@ -1648,7 +1832,10 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
   Work &wk = device_work(dev);
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
-  const int waves = split ? x3::WAVES : (pf ? 8 : 4);
+  // the choice heads' nets (up to 31 inputs) on the split-precision kernel too (wider: f32 MFMA)
+  const bool split_c = !pf && !exact && n_in <= 31;
+  if (split_c && ((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
+  const int waves = (split || split_c) ? x3::WAVES : (pf ? 8 : 4);
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
   const int64_t tiles = (M + 31) / 32;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (tiles + waves - 1) / waves));
@@ -1656,12 +1843,20 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   if (!ensure_work(wk, nw)) return set_error(MHPPO_ENOMEM, "mlp_train partials");
   const dim3 grid((unsigned)blocks);
 #define MLP_ARGS grid, s, packed, X, n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d
-  if (split) {
-#define X3_LAUNCH(KIND_)                                                                                    \
-  hipLaunchKernelGGL((k_mlp_train_x3<KIND_>), grid, dim3(64 * x3::WAVES), x3::LDS_BYTES, s, packed, X, M, ret, value, \
-                     act, logp_old, stats, m_global, out_mean, out_std, wk.g, wk.d)
-    if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC);
-    else X3_LAUNCH(K_CONT);
+  if (split || split_c) {
+#define X3_LAUNCH(KIND_, G_)                                                                                 \
+  hipLaunchKernelGGL((k_mlp_train_x3<KIND_, x3::G_>), grid, dim3(64 * x3::WAVES), x3::G_::LDS_BYTES, s, packed, X, \
+                     n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d)
+    if (split) {
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, G13);
+      else X3_LAUNCH(K_CONT, G13);
+    } else if (n_in <= 15) {
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV16);
+      else X3_LAUNCH(K_CHOICE, GC16);
+    } else {
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV32);
+      else X3_LAUNCH(K_CHOICE, GC32);
+    }
 #undef X3_LAUNCH
   } else if (pf) {
     if (kind == K_CRITIC)
@@ -1721,7 +1916,7 @@ extern "C" int mhppo_mlp_train_pair(const float *packed_actor, const float *pack
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(wk.cus, (tiles + x3::WAVES - 1) / x3::WAVES));
   const int nw = (int)blocks * x3::WAVES;
   if (!ensure_work(wk, 2 * nw)) return set_error(MHPPO_ENOMEM, "mlp_train partials");
-  hipLaunchKernelGGL(k_mlp_train_x3_pair, dim3((unsigned)blocks), dim3(64 * x3::WAVES), x3::LDS_BYTES_PAIR, s,
+  hipLaunchKernelGGL(k_mlp_train_x3_pair, dim3((unsigned)blocks), dim3(64 * x3::WAVES), x3::G13::LDS_BYTES_PAIR, s,
                      packed_actor, packed_critic, X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std,
                      wk.g, wk.d);
   // the two nets' partials (actor waves [0, nw), critic waves [nw, 2 nw)) in one launch pair

@@ -189,7 +189,7 @@ class Algo_PPO:
         # lane fix is an env option: VecCrosswalk(..., fix_scalable_lanes=True).
         self.fix_bucket = False
         self.fix_choice_loss = False
-        # continuous heads trained on the exact f32-MFMA kernel (k-ordered fmaf sums) instead of the
+        # all heads trained on the exact f32-MFMA kernel (k-ordered fmaf sums) instead of the
         # default bf16x3 split-precision one (f32-level products at 2.67x the f32-MFMA ceiling)
         self.exact_f32 = False
         # reward curves written to load_model/parameters at the end of train() (:908-916)
@@ -229,7 +229,7 @@ class Algo_PPO:
             if m_d > 0:  # never empty in the reference (>= 1 existing car per episode); it would raise there
                 heads.append(ppo.Head("d", self.actor_net_choice, self.critic_net_choice, self.optimizer_actor_choice,
                                       self.optimizer_critic_choice, d["obs"], d["act"], d["logp"], d["ret"], m_d,
-                                      counts, per_row=self.fix_choice_loss))
+                                      counts, per_row=self.fix_choice_loss, exact=self.exact_f32))
                 names.append("choice")
             losses = ppo.train_epochs(heads, 10, self.grad_bucket) if heads else None
         if self.verbose and losses is not None:

@@ -192,7 +192,7 @@ FLOPS_PER_ROW_CONT = flops_per_row(13, 1)
 N_IN_MAX = 64  # the fused kernel's widest input (scalable 8-slot choice head: dc = 54)
 
 KIND_CRITIC, KIND_CONT, KIND_CHOICE = 0, 1, 2
-# MHPPO_TRAIN_EXACT_F32 (include/mhppo.h mhppo_mlp_train): the 13-input heads' passes on the f32-MFMA
+# MHPPO_TRAIN_EXACT_F32 (include/mhppo.h mhppo_mlp_train): a head's passes on the f32-MFMA
 # kernel (k-ordered fmaf sums, the exact f32 arithmetic of an fmaf chain) instead of the default
 # bf16x3 split-precision one; per head: Head(exact=True), set by Algo_PPO(exact_f32=True)
 TRAIN_EXACT_F32 = 0x100
@@ -211,8 +211,8 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient.
     `sums`: optional zeroed float64 [3] the kernel accumulates into (train_epoch passes rows of
     one zeroed tensor: one fill per epoch instead of one per pass).
-    exact: the f32-MFMA kernel instead of the split-precision one (13-input heads; the choice
-    heads always run on f32 MFMA)."""
+    exact: the f32-MFMA kernel instead of the split-precision one (any head with n_in <= 31;
+    wider choice heads always run on f32 MFMA)."""
     want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
     if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):
         raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
@@ -289,8 +289,8 @@ class Head:
     """One actor/critic pair, its Adam optimisers and this rank's shard of its batch.
     kind "c": continuous head (train_model_c, :778-815); "d": choice head (train_model_d,
     :818-851) with the GLOBAL action counts (n0, n1) of the M x M broadcast, or the
-    opt-in per-row loss.  m = the global row count.  exact: the continuous head's
-    passes on the exact f32-MFMA kernel (Algo_PPO(exact_f32=True))."""
+    opt-in per-row loss.  m = the global row count.  exact: the head's passes on
+    the exact f32-MFMA kernel (Algo_PPO(exact_f32=True))."""
 
     def __init__(self, kind, actor, critic, opt_actor, opt_critic, obs, act, logp, ret, m, counts=None,
                  per_row=False, exact=False):
@@ -320,9 +320,10 @@ def train_epoch(heads, bucket=None):
             k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V, h.act, h.logp, st, m_global=h.m, sums=sa, exact=h.exact)
         elif h.per_row:
             k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, h.act.float(), h.logp, st, None, m_global=h.m,
-                        sums=sa)
+                        sums=sa, exact=h.exact)
         else:
-            k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, None, h.logp, st, h.counts, m_global=h.m, sums=sa)
+            k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V, None, h.logp, st, h.counts, m_global=h.m, sums=sa,
+                        exact=h.exact)
         out.append((sa[0:1], sc[0:1]))
     nets = [n for h in heads for n in (h.actor, h.critic)]
     if bucket is not None:
@@ -383,10 +384,10 @@ def train_epochs(heads, n_epochs, bucket=None):
                                 exact=h.exact)
                 elif h.per_row:
                     k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], h.act.float(), h.logp, st, None,
-                                m_global=h.m, sums=sa)
+                                m_global=h.m, sums=sa, exact=h.exact)
                 else:
                     k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], None, h.logp, st, h.counts, m_global=h.m,
-                                sums=sa)
+                                sums=sa, exact=h.exact)
                 trained.append(h.actor)
                 out[i][0] = sa[0:1]
             if crit:  # the critic pass of epoch k
@@ -519,9 +520,11 @@ def train_model_c(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret,
                              exact=exact)])[0]
 
 
-def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row=False):
+def train_model_d(actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row=False,
+                  exact=False):
     """One full-batch epoch of Algo_PPO.train_model_d (:818-851) for one head: O(M) form of
     the M x M Categorical surrogate with the global action counts (n0, n1); per_row=True is
     the opt-in bug fix.  Returns this rank's (actor, critic) loss sums."""
-    h = Head("d", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row)
+    h = Head("d", actor, critic, opt_actor, opt_critic, obs, act, logp_old, ret, m_global, counts, per_row,
+             exact=exact)
     return train_epoch([h])[0]

@@ -95,8 +95,8 @@ def _close_grad(g, gt):
     torch.testing.assert_close(g, gt, rtol=0, atol=1e-4 * float(gt.abs().max()) + 1e-9)
 
 
-def _critic_pass(ppo, critic, obs, ret, m):
-    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m)
+def _critic_pass(ppo, critic, obs, ret, m, exact=False):
+    gc, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m, exact=exact)
     Vt = torch.squeeze(critic(obs), -1)
     torch.testing.assert_close(V, Vt.detach(), rtol=1e-5, atol=1e-5)
     dv, lc = ppo.k_mse(Vt, ret, m)
@@ -133,12 +133,15 @@ def test_fused_cont_grads_vs_autograd(M):
     _close_grad(ga, gat)
 
 
-@pytest.mark.parametrize("M,dc", [(1, 12), (45, 17), (4096, 27), (20001, 30), (333, 32), (70, 54), (65536, 54),
-                                  (1000, 40), (257, 64)])
-def test_fused_choice_grads_vs_autograd(M, dc):
+@pytest.mark.parametrize("M,dc,exact", [(1, 12, False), (45, 17, False), (4096, 27, False), (20001, 30, False),
+                                        (333, 32, False), (70, 54, False), (65536, 54, False), (1000, 40, False),
+                                        (257, 64, False), (20001, 30, True), (4097, 16, True), (100003, 17, False),
+                                        (64, 16, False), (65, 31, False)])
+def test_fused_choice_grads_vs_autograd(M, dc, exact):
     """mhppo_mlp_train kinds 0/2 on choice-head shapes (dc = 12..64 inputs — 54 is the
     scalable 8-slot driver's choice head, 2-way softmax, O(M) count-weighted surrogate) vs
-    torch autograd + the HIP choice-loss kernel."""
+    torch autograd + the HIP choice-loss kernel.  dc <= 31 runs on the bf16x3 split kernel
+    (K = 16 / 32 geometries), exact=True and dc > 31 on the f32-MFMA one."""
     from mhppo import ppo
     from mhppo.models import Model_PPO
     torch.manual_seed(M + dc)
@@ -150,8 +153,8 @@ def test_fused_choice_grads_vs_autograd(M, dc):
     lp = torch.log(torch.rand(M) * 0.8 + 0.1).cuda()
     m = float(M) if M > 1 else 2.0
     counts = torch.tensor([float((act == 0).sum()), float((act == 1).sum())], dtype=torch.float64).cuda()
-    Vt, st = _critic_pass(ppo, critic, obs, ret, m)
-    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CHOICE, actor, obs, ret, Vt, None, lp, st, counts, m_global=m)
+    Vt, st = _critic_pass(ppo, critic, obs, ret, m, exact)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CHOICE, actor, obs, ret, Vt, None, lp, st, counts, m_global=m, exact=exact)
     probs = actor(obs).reshape(-1, 2)
     adv = ppo.k_adv_normalize(ret, Vt, st, m)
     dp, la = ppo.k_ppo_choice(probs, lp, adv, counts, m)

@@ -16,6 +16,8 @@ ap.add_argument("--rows", type=int, default=10485760)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--exact", action="store_true", help="the exact f32-MFMA kernel (MHPPO_TRAIN_EXACT_F32)")
 ap.add_argument("--pair", action="store_true", help="also time the fused actor+critic launch (mhppo_mlp_train_pair)")
+ap.add_argument("--choice", type=int, default=0, help="also time a choice head with this many inputs, split vs exact")
+ap.add_argument("--choice-rows", type=int, default=655360)
 a = ap.parse_args()
 M = a.rows
 torch.manual_seed(0)
@@ -55,4 +57,28 @@ if a.pair:
     ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
     tf = 2 * ppo.FLOPS_PER_ROW_CONT * M / (ms * 1e-3) / 1e12
     print(f"pair rows {M}: {ms:.3f} ms (both passes)  {tf:.1f} TFLOP/s", flush=True)
+if a.choice:
+    dc, Mc = a.choice, a.choice_rows
+    ca = Model_PPO(dc, 2, 2).cuda()
+    cc = Model_PPO(dc, 1, 0).cuda()
+    xo = torch.randn(Mc, dc, device="cuda") * 2
+    xr = torch.randn(Mc, device="cuda") * 3 - 5
+    xa = (torch.rand(Mc, device="cuda") < 0.4).float()
+    xl = torch.log(torch.rand(Mc, device="cuda") * 0.8 + 0.1)
+    cnt = torch.stack([(xa == 0).sum(), (xa == 1).sum()]).double()
+    flops = 6 * (dc * 32 + 32 * 64 + 64 * 32 + 32 * 2)  # fwd + bwd(dX, dW) multiply-adds x 2
+    for exact in (False, True):
+        for kind in (0, 2):
+            ppo.TRAIN_EVENTS = []
+            for r in range(a.reps + 2):
+                if r == 2:
+                    torch.cuda.synchronize()
+                    ppo.TRAIN_EVENTS = []
+                _, scc, Vc = ppo.k_mlp_train(0, cc, xo, xr, m_global=float(Mc), exact=exact) if kind == 0 else (0, scc, Vc)
+                if kind == 2:
+                    ppo.k_mlp_train(2, ca, xo, xr, Vc, None, xl, scc[1:3].clone(), cnt, m_global=float(Mc), exact=exact)
+            torch.cuda.synchronize()
+            ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps
+            print(f"choice dc {dc} kind {kind} {'exact' if exact else 'split'} rows {Mc}: {ms:.4f} ms "
+                  f"{flops * Mc / (ms * 1e-3) / 1e12:.1f} TFLOP/s", flush=True)
 ppo.TRAIN_EVENTS = None
