@@ -96,7 +96,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
                     help="BASELINE.json config: 3 = 4cars 4/1/2 (the metric), 4 = scalable 8/1/4, 2 = coop 2/1/2")
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None,
+                    help="envs per GPU (default: BASELINE.json's for the config: 4096 for config 2, else 65536)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=4096)
     ap.add_argument("--dist-backend", default="nccl",
@@ -183,6 +184,8 @@ def main():
     global CONFIG
     CONFIG = a.config
     variant, nc, npd, nl = CONFIGS[a.config]
+    if a.envs is None:
+        a.envs = 4096 if a.config == 2 else 65536
     N, T = a.envs, 80
     venv = VecCrosswalk(variant, N, nc, npd, nl, seed_base=0, env_id_offset=rank * N, device=f"cuda:{local}")
     torch.manual_seed(0)
@@ -222,23 +225,31 @@ def main():
     # (RolloutGPU.parts), from torch events around whole collects.
     gpu = algo.rollout.gpu
     env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
-    step_us = {}
+    step_us, fused_kern_us = {}, None
+    modes = [("one_chain", 1, False)] + ([("parts", gpu.parts, False)] if gpu.parts > 1 else []) + \
+        ([("fused", 1, True)] if gpu.fused_ok else [])
     with torch.no_grad():
-        for parts in sorted({1, gpu.parts}):
+        for name, parts, fused in modes:
             algo.rollout.reset()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            if parts == 1:
+            timed = name in ("one_chain", "fused")
+            if timed:
                 _lib.check(L.mhppo_kernel_timing_begin(T))
             e0.record()
             gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=7, iteration=0,
-                        parts=parts)
+                        parts=parts, fused=fused)
             e1.record()
             torch.cuda.synchronize()
-            if parts == 1:
-                _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(env_ms), ctypes.byref(env_n)))
-            step_us[parts] = e0.elapsed_time(e1) * 1e3 / T
-    if env_n.value != T:
-        raise RuntimeError(f"timed {env_n.value} env-step launches, expected {T}")
+            if timed:
+                ms_, n_ = ctypes.c_double(0.0), ctypes.c_int32(0)
+                _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(ms_), ctypes.byref(n_)))
+                if n_.value != T:
+                    raise RuntimeError(f"timed {n_.value} step launches, expected {T}")
+                if fused:
+                    fused_kern_us = ms_.value / T * 1e3
+                else:
+                    env_ms, env_n = ms_, n_
+            step_us[name] = e0.elapsed_time(e1) * 1e3 / T
     kern_ms = env_ms.value / env_n.value
     S = venv.n_slots
     S_all = 2 * S if variant == "4cars" else S  # car slots incl. the 4cars IDM followers
@@ -285,9 +296,12 @@ def main():
                          "bytes_per_launch": per_env * N, "bytes_per_env_step": per_env,
                          "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3),
                          "measured_on": "one extra 80-step rollout after the timed region, all N envs per launch"},
-        "rollout_step_us": {"one_chain": step_us[1], "parts": gpu.parts, "product": step_us[gpu.parts],
-                            "note": "wall time per rollout step (policy + env step launches), torch events around "
-                                    "a whole 80-step collect"},
+        "rollout_step_us": {**step_us, "parts_n": gpu.parts, "fused_kernel": fused_kern_us,
+                            "product": step_us["fused" if gpu.fused else ("parts" if gpu.parts > 1 else "one_chain")],
+                            "note": "wall time per rollout step, torch events around a whole 80-step collect: "
+                                    "one_chain = policy + env-step launches, parts = those on two streams "
+                                    "(env halves), fused = one launch per step (mhppo_rollout_step_fused; "
+                                    "fused_kernel = its dispatch-attached kernel time)"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)

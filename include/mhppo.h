@@ -216,6 +216,16 @@ int mhppo_rollout_policy_part(mhppo_env *env, const mhppo_mlp *actor_cross, cons
 int mhppo_rollout_sample_env_part(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, int part,
                                   void *stream);
 
+/* Step t as ONE launch (one pedestrian per env, a compiled register-view shape: configs 2, 3
+ * and 4): each wave runs the cross / wait actors for its envs' rows on f32 MFMA (the rows
+ * compacted by head per wave) and then the sample / env step with the outputs in registers.
+ * Results are bit-identical to mhppo_rollout_policy + mhppo_rollout_sample_env; feat_c must
+ * point at obs_c + t*N*S*13; rows and parts are not used.  mhppo_rollout_fused_supported
+ * returns 1 when the env's shape has the kernel, else 0 (then this returns MHPPO_EINVAL). */
+int mhppo_rollout_fused_supported(const mhppo_env *env);
+int mhppo_rollout_step_fused(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                             const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
+
 /* Measurement (bench.py): the next `n` env-step launches (mhppo_rollout_sample_env) of the
  * calling thread on the device current at this call carry HIP events attached to their dispatch
  * packets (hipExtLaunchKernelGGL start/stop events: the kernel's execution, not the queue's

@@ -1630,6 +1630,24 @@ __device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int
   }
   MHPPO_MARK_FLUSH();
 }
+// The four waves' gradient partials folded per block through LDS (fixed order, float64): one
+// float64 partial per block, a quarter of the per-wave partials' bytes for the two-stage
+// reduction to write and read.  The weight images and tile slots are dead once every wave has
+// left its tile loop (the first barrier); the second publishes the four partials.
+template <class G, class PassT>
+__device__ __forceinline__ void fold_partials(PassT &p, const WaveSlot<G> &ws, char *L8, int w, int tid, int np,
+                                              double *__restrict__ gblk, double *__restrict__ dblk) {
+  static_assert(WAVES * Packed(G::K1 - 1, G::NOUT).NP * 4 + 8 + WAVES * 3 * 8 <= G::LDS_BYTES,
+                "the four partials fit the kernel's LDS");
+  __syncthreads();
+  float *part = reinterpret_cast<float *>(L8);
+  double *dl = reinterpret_cast<double *>(L8 + (WAVES * np * 4 + 7) / 8 * 8);
+  p.finish(ws, part + w * np, dl + w * 3);
+  __syncthreads();
+  for (int k = tid; k < np; k += 64 * WAVES)
+    gblk[k] = (((double)part[k] + (double)part[np + k]) + (double)part[2 * np + k]) + (double)part[3 * np + k];
+  if (tid < 3) dblk[tid] = ((dl[tid] + dl[3 + tid]) + dl[6 + tid]) + dl[9 + tid];
+}
 }  // namespace x3
 
 template <int KIND, class G>
@@ -1638,7 +1656,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
                    const float *__restrict__ ret, float *__restrict__ V, const float *__restrict__ act,
                    const float *__restrict__ lp_old, const double *__restrict__ stats,
                    const double *__restrict__ counts, double m_global, float out_mean, float out_std,
-                   float *__restrict__ gpart, double *__restrict__ dpart) {
+                   double *__restrict__ gpart, double *__restrict__ dpart) {
   using namespace x3;
   extern __shared__ float lds[];
   char *L8 = reinterpret_cast<char *>(lds);
@@ -1658,7 +1676,8 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   tile_loop<KIND, G>(ws, gw, nw, M, X, nin, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
     p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
   });
-  p.finish(ws, gpart + (size_t)gw * Packed(geo_nin<G>(nin), G::NOUT).NP, dpart + gw * 3);
+  const int np = Packed(geo_nin<G>(nin), G::NOUT).NP;
+  fold_partials<G>(p, ws, L8, w, tid, np, gpart + (size_t)blockIdx.x * np, dpart + blockIdx.x * 3);
 }
 
 // Actor pass of epoch e fused with the critic pass of epoch e + 1 (Algo_PPO.train_model_c
@@ -1677,7 +1696,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
                         int64_t M, const float *__restrict__ ret, float *__restrict__ V,
                         const float *__restrict__ act, const float *__restrict__ lp_old,
                         const double *__restrict__ stats, double m_global, float out_mean, float out_std,
-                        float *__restrict__ gpart, double *__restrict__ dpart) {
+                        double *__restrict__ gpart, double *__restrict__ dpart) {
   using namespace x3;
   extern __shared__ float lds[];
   char *L8 = reinterpret_cast<char *>(lds);
@@ -1701,8 +1720,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
     pc.tile(ws, slot, row0, nrows, V, 0.f, 1.f, inv_m, out_mean, out_std);
   });
   constexpr int NWP = Packed(NIN_CONT, 1).NP;
-  pa.finish(ws, gpart + (size_t)gw * NWP, dpart + gw * 3);
-  pc.finish(ws, gpart + (size_t)(nw + gw) * NWP, dpart + (nw + gw) * 3);
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  fold_partials<G>(pa, ws, L8, w, tid, NWP, gpart + (size_t)b * NWP, dpart + b * 3);
+  fold_partials<G>(pc, ws, L8, w, tid, NWP, gpart + (size_t)(nb + b) * NWP, dpart + (nb + b) * 3);
 }
 
 
@@ -1711,10 +1731,12 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
 // Slot k < np is gradient k, slots np..np+2 the float64 sums.
 constexpr int RG = 64;
 
-// blockIdx.z = net: a fused pair launch reduces both nets' partials (net z's waves follow net
+// blockIdx.z = net: a fused pair launch reduces both nets' partials (net z's partials follow net
 // z - 1's in gpart / dpart; its group totals at tmp + z RG (np + 3)) in the same two launches.
+// Partials: float per wave (the f32 kernel), float64 per block (the split kernel's LDS fold).
+template <class T>
 __global__ void __launch_bounds__(256)
-    k_grad_stage1(const float *gpart, const double *dpart, int nw, int np, double *tmp) {
+    k_grad_stage1(const T *gpart, const double *dpart, int nw, int np, double *tmp) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   const int g = blockIdx.y, nd = np + 3, z = blockIdx.z;
   gpart += (size_t)z * nw * np;
@@ -1846,7 +1868,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   if (split || split_c) {
 #define X3_LAUNCH(KIND_, G_)                                                                                 \
   hipLaunchKernelGGL((k_mlp_train_x3<KIND_, x3::G_>), grid, dim3(64 * x3::WAVES), x3::G_::LDS_BYTES, s, packed, X, \
-                     n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std, wk.g, wk.d)
+                     n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std,                 \
+                     reinterpret_cast<double *>(wk.g), wk.d)
     if (split) {
       if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, G13);
       else X3_LAUNCH(K_CONT, G13);
@@ -1884,7 +1907,12 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   }
 #undef MLP_ARGS
   const int np = n_params(n_in, kind == K_CHOICE ? 2 : 1);
-  hipLaunchKernelGGL(k_grad_stage1, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, np, wk.t);
+  if (split || split_c)  // one float64 partial per block
+    hipLaunchKernelGGL(k_grad_stage1<double>, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s,
+                       reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, wk.t);
+  else  // one float partial per wave
+    hipLaunchKernelGGL(k_grad_stage1<float>, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, np,
+                       wk.t);
   hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums, nullptr,
                      nullptr);
   CHECK_HIP(hipGetLastError());
@@ -1918,9 +1946,10 @@ extern "C" int mhppo_mlp_train_pair(const float *packed_actor, const float *pack
   if (!ensure_work(wk, 2 * nw)) return set_error(MHPPO_ENOMEM, "mlp_train partials");
   hipLaunchKernelGGL(k_mlp_train_x3_pair, dim3((unsigned)blocks), dim3(64 * x3::WAVES), x3::G13::LDS_BYTES_PAIR, s,
                      packed_actor, packed_critic, X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std,
-                     wk.g, wk.d);
-  // the two nets' partials (actor waves [0, nw), critic waves [nw, 2 nw)) in one launch pair
-  hipLaunchKernelGGL(k_grad_stage1, dim3((np + 3 + 255) / 256, RG, 2), dim3(256), 0, s, wk.g, wk.d, nw, np, wk.t);
+                     reinterpret_cast<double *>(wk.g), wk.d);
+  // the two nets' block partials (actor [0, blocks), critic [blocks, 2 blocks)) in one launch pair
+  hipLaunchKernelGGL(k_grad_stage1<double>, dim3((np + 3 + 255) / 256, RG, 2), dim3(256), 0, s,
+                     reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, wk.t);
   hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256, 1, 2), dim3(256), 0, s, wk.t, np, grad_actor,
                      sums_actor, grad_critic, sums_critic);
   CHECK_HIP(hipGetLastError());

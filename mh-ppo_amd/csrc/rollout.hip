@@ -277,6 +277,45 @@ __device__ __forceinline__ void stage_both(float *L, const float *__restrict__ W
     if (tid == 0) Lh[O_B4] = vb4[h];
   }
 }
+// One 32-row tile of one 13 -> 32 -> 64 -> 32 -> 1 actor (Wl: its LDS image above) on f32 MFMA:
+// lane j of both halves holds row j's features f; returns the row's pre-tanh output in every
+// lane — the oracle's ascending fmaf chains bit for bit (the permuted staging).
+__device__ __forceinline__ float actor_tile(const float *Wl, const float (&f)[NF_C + 1], int j, int kh) {
+  f32x16 h1 = zero16();
+#pragma unroll
+  for (int s = 0; s < 7; s++) {
+    // both lane halves hold the row's features: the lower half takes f[2s], the upper f[2s + 1]
+    // (one v_permlane32_swap; a lane-select of the two is folded into an indexed load of f,
+    // which puts f in scratch memory)
+    const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(f[2 * s]), __float_as_uint(f[2 * s + 1]), false, false);
+    h1 = mfma(Wl[O_W1 + j * S1 + 2 * s + kh], __uint_as_float(x[0]), h1);
+  }
+  bias_relu(h1, Wl + O_B1, kh);
+  f32x16 h2a = zero16(), h2b = zero16();
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    h2a = mfma(Wl[O_W2 + j * S2 + 2 * s + kh], h1[s], h2a);
+    h2b = mfma(Wl[O_W2 + (32 + j) * S2 + 2 * s + kh], h1[s], h2b);
+  }
+  bias_relu(h2a, Wl + O_B2, kh);
+  bias_relu(h2b, Wl + O_B2 + 32, kh);
+  f32x16 h3 = zero16();
+#pragma unroll
+  for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 2 * s + kh], h2a[s], h3);
+#pragma unroll
+  for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 32 + 2 * s + kh], h2b[s], h3);
+  bias_relu(h3, Wl + O_B3, kh);
+  float y = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    // neuron 2s sits in register s of the lower lane half, 2s + 1 in the upper: one
+    // v_permlane32_swap gives every lane both (r[0] = neuron 2s, r[1] = neuron 2s + 1 of its row)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(h3[s]), __float_as_uint(h3[s]), false, false);
+    y = fmaf(Wl[O_W4 + 2 * s], __uint_as_float(r[0]), y);
+    y = fmaf(Wl[O_W4 + 2 * s + 1], __uint_as_float(r[1]), y);
+  }
+  return y + Wl[O_B4];
+}
 }  // namespace pol
 
 template <int V>
@@ -350,40 +389,7 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
 #pragma unroll
       for (int q = 0; q < NF_C; q++) fo[q] = f[q];
     }
-    f32x16 h1 = zero16();
-#pragma unroll
-    for (int s = 0; s < 7; s++) {
-      // both lane halves hold the row's features: the lower half takes f[2s], the upper f[2s + 1]
-      // (one v_permlane32_swap; a lane-select of the two is folded into an indexed load of f,
-      // which puts f in scratch memory)
-      const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(f[2 * s]), __float_as_uint(f[2 * s + 1]), false, false);
-      h1 = mfma(Wl[O_W1 + j * S1 + 2 * s + kh], __uint_as_float(x[0]), h1);
-    }
-    bias_relu(h1, Wl + O_B1, kh);
-    f32x16 h2a = zero16(), h2b = zero16();
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-      h2a = mfma(Wl[O_W2 + j * S2 + 2 * s + kh], h1[s], h2a);
-      h2b = mfma(Wl[O_W2 + (32 + j) * S2 + 2 * s + kh], h1[s], h2b);
-    }
-    bias_relu(h2a, Wl + O_B2, kh);
-    bias_relu(h2b, Wl + O_B2 + 32, kh);
-    f32x16 h3 = zero16();
-#pragma unroll
-    for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 2 * s + kh], h2a[s], h3);
-#pragma unroll
-    for (int s = 0; s < 16; s++) h3 = mfma(Wl[O_W3 + j * S3 + 32 + 2 * s + kh], h2b[s], h3);
-    bias_relu(h3, Wl + O_B3, kh);
-    float y = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-      // neuron 2s sits in register s of the lower lane half, 2s + 1 in the upper: one
-      // v_permlane32_swap gives every lane both (r[0] = neuron 2s, r[1] = neuron 2s + 1 of its row)
-      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(h3[s]), __float_as_uint(h3[s]), false, false);
-      y = fmaf(Wl[O_W4 + 2 * s], __uint_as_float(r[0]), y);
-      y = fmaf(Wl[O_W4 + 2 * s + 1], __uint_as_float(r[1]), y);
-    }
-    const float out = y + Wl[O_B4];
+    const float out = actor_tile(Wl, f, j, kh);
     if (valid && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)
       const float t = mhppo_tanhf(out) * (head ? std_w : std_c);  // Model_PPO type 1 (:87-89)
       B.out_c[r] = t + (head ? mean_w : mean_c);
@@ -451,9 +457,11 @@ __global__ void __launch_bounds__(TPB) k_head_place(const int32_t *a_d, int R, c
 // one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min.
 // All of this lane's rollout inputs are read before any buffer write so the loads
 // issue as one batch; EV is the generic or the register env view.
-template <class EV>
+template <class EV, bool REG_OUT = false>
 __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__ eps, int t,
-                                                const mhppo_rollout_bufs &B) {
+                                                const mhppo_rollout_bufs &B, const float *outr = nullptr) {
+  // REG_OUT (the fused step, one pedestrian): slot i's actor output is outr[i], not out_c
+  static_assert(!REG_OUT || EV::CNP == 1, "register outputs: one pedestrian");
   constexpr int V = EV::VAR;
   const Cfg &c = E.c;
   const int e = E.e;
@@ -484,7 +492,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
       if constexpr (V == V_SCALABLE) {
         if (EV::CNP > 0 ? !(E.pflag(p) & F_EXIST) : o[L.ped_off + p * 9 + 7] == 0.0f) continue;
       }
-      float out = B.out_c[row0 + p];
+      float out = REG_OUT ? outr[i] : B.out_c[row0 + p];
       loc = t_minimum(loc, out);
       if (out == loc) sel = p;
     }
@@ -589,6 +597,104 @@ __global__ void __launch_bounds__(TPB)
     g_wave_times[2 * wv + 1] = wt1;
   }
 #endif
+}
+
+// -------------------------------------------------------------- fused step (one pedestrian)
+// The whole rollout step in one launch (Env_rollout.iterations_rand :430-461 policy forward, then
+// the sample / env.step of k_sample_env_r): each wave first runs the cross / wait actors for its
+// 64 envs' S rows — k_policy_mfma's 32-row f32-MFMA tiles (actor_tile: the same bits), the rows
+// compacted by head in LDS per wave (cross rows, then wait rows from the next 32-row boundary,
+// so each tile is one actor) — then sample_env_body on the register env view takes the outputs
+// from registers.  Saves the policy launch and its out_c round trip; the tile-0 gathers and the
+// env-state loads are issued before the first tile, so they land under the MFMA work.
+template <int V, int NC, int NAV, int NP>
+__global__ void __launch_bounds__(TPB)
+    k_step_fused(Cfg c, Bufs eb, const float *__restrict__ Wc, const float *__restrict__ Ww, float mean_c,
+                 float std_c, float mean_w, float std_w, const float *eps, int t, mhppo_rollout_bufs B, int e_lo,
+                 int e_hi) {
+  using namespace pol;
+  using EV = EnvR<V, NC, NAV, NP>;
+  constexpr int S = EV::CNS, ROWS = 64 * S + 32;
+  static_assert(NP == 1 && S > 0, "fused step: one pedestrian, compile-time slots");
+  extern __shared__ float lds[];  // [2][HEAD] actors | per wave: row list [ROWS] | outputs [ROWS]
+  const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5, w = tid >> 6;
+  int *list = reinterpret_cast<int *>(lds + 2 * HEAD) + w * 2 * ROWS;
+  float *outs = reinterpret_cast<float *>(list + ROWS);
+  const int e = e_lo + blockIdx.x * TPB + tid;
+  const bool act = e < e_hi;
+  int ad[S];  // this lane's rows' choices (cross when 0: k_head_count), fixed for the episode
+#pragma unroll
+  for (int i = 0; i < S; i++) ad[i] = act ? B.a_d[(size_t)e * S + i] : 1;
+  stage_both<TPB>(lds, Wc, Ww, tid);
+  // per-wave compaction: cross rows at [0, nc), wait rows at [32 tc, 32 tc + nw)
+  const uint64_t below = l ? (~0ull >> (64 - l)) : 0ull;
+  int pos[S], nc = 0, nw = 0;
+#pragma unroll
+  for (int i = 0; i < S; i++) {
+    const uint64_t m = __ballot(act && ad[i] == 0);
+    pos[i] = nc + __popcll(m & below);
+    nc += __popcll(m);
+  }
+  const int tc = (nc + 31) / 32;
+#pragma unroll
+  for (int i = 0; i < S; i++) {
+    const uint64_t m = __ballot(act && ad[i] != 0);
+    if (ad[i] != 0) pos[i] = 32 * tc + nw + __popcll(m & below);
+    nw += __popcll(m);
+  }
+#pragma unroll
+  for (int i = 0; i < S; i++)
+    if (act) list[pos[i]] = e * S + i;  // the global row (env, slot), P = 1
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int ntiles = tc + (nw + 31) / 32, wend = 32 * tc + nw;
+  const ObsLayout L = obs_layout(c);
+  auto tile_raw = [&](int tl, int &r, bool &ok) {
+    const int p0 = 32 * tl + j;
+    ok = tl < tc ? p0 < nc : p0 < wend;
+    r = list[ok ? p0 : 32 * tl];  // an invalid lane gathers its tile's first (valid) row
+    const int ee = r / S;
+    return feat_raw(B.obs + (size_t)ee * L.obs_dim, L, r - ee * S, 0);
+  };
+  int r_cur = 0;
+  bool ok_cur = false;
+  FeatRaw raw_cur;
+  if (ntiles > 0) raw_cur = tile_raw(0, r_cur, ok_cur);
+  EV E(c, eb, act ? e : e_lo);  // the env-state loads, in flight under the tiles (a spare lane: a valid env)
+  __syncthreads();              // both actors staged
+  for (int tile = 0; tile < ntiles; tile++) {
+    int r_nxt = r_cur;
+    bool ok_nxt = false;
+    FeatRaw raw_nxt = raw_cur;
+    if (tile + 1 < ntiles) raw_nxt = tile_raw(tile + 1, r_nxt, ok_nxt);
+    const int head = tile >= tc;
+    float f[NF_C + 1];
+    const float ex = obs_car_ped_raw(raw_cur, f);
+    f[NF_C] = 0.0f;
+    if (ok_cur && kh == 0) {
+      float *fo = B.feat_c + (size_t)r_cur * NF_C;
+#pragma unroll
+      for (int q = 0; q < NF_C; q++) fo[q] = f[q];
+    }
+    const float out = actor_tile(lds + head * HEAD, f, j, kh);
+    if (ok_cur && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)
+      const float tv = mhppo_tanhf(out) * (head ? std_w : std_c) + (head ? mean_w : mean_c);
+      B.out_c[r_cur] = tv;
+      outs[32 * tile + j] = tv;
+    }
+    r_cur = r_nxt;
+    ok_cur = ok_nxt;
+    raw_cur = raw_nxt;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!act) return;
+  float outr[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) outr[i] = outs[pos[i]];  // a gated row's value is never read
+  sample_env_body<EV, true>(E, eps, t, B, outr);
 }
 
 // -------------------------------------------------------------- evaluation
@@ -1045,6 +1151,33 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
   }
 }
 
+// the fused step for a compiled one-pedestrian shape (false: no such kernel; 4cars2 has no driver)
+template <int V, int NC, int NAV, int NP>
+bool launch_step_fused(const Cfg &c, const Bufs &eb, const mhppo_mlp &mc, const mhppo_mlp &mw, const float *eps, int t,
+                       const mhppo_rollout_bufs &B, hipStream_t s) {
+  if constexpr (V == V_4CARS2 || NP != 1) {
+    return false;
+  } else {
+    if (!use_reg_view(c, V, NC, NAV, NP)) return false;
+    constexpr int ROWS = 64 * EnvR<V, NC, NAV, NP>::CNS + 32;
+    const size_t shm = sizeof(float) * (2 * pol::HEAD + (TPB / 64) * 2 * ROWS);
+    const dim3 g = grid_for((size_t)c.N);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ktime_next(e0, e1))
+      hipExtLaunchKernelGGL((k_step_fused<V, NC, NAV, NP>), g, dim3(TPB), shm, s, e0, e1, 0, c, eb, mc.packed,
+                            mw.packed, mc.mean, mc.std, mw.mean, mw.std, eps, t, B, 0, c.N);
+    else
+      hipLaunchKernelGGL((k_step_fused<V, NC, NAV, NP>), g, dim3(TPB), shm, s, c, eb, mc.packed, mw.packed, mc.mean,
+                         mc.std, mw.mean, mw.std, eps, t, B, 0, c.N);
+    return true;
+  }
+}
+template <int V, int NC, int NAV, int NP>
+bool has_step_fused(const Cfg &c) {
+  if constexpr (V == V_4CARS2 || NP != 1) return false;
+  else return use_reg_view(c, V, NC, NAV, NP);
+}
+
 // Env range of part `part` of `nparts` (the two-stream rollout, RolloutGPU(parts=2)): boundaries at
 // multiples of 64 envs (whole waves), the last part ends at N
 __host__ __device__ inline int part_env(const Cfg &c, int part, int nparts) {
@@ -1284,6 +1417,38 @@ int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo
   int rc = mhppo_rollout_policy(env, actor_cross, actor_wait, bufs, stream);
   if (rc) return rc;
   return mhppo_rollout_sample_env(env, eps, t, bufs, stream);
+}
+
+int mhppo_rollout_fused_supported(const mhppo_env *env) {
+  if (!env) return set_error(MHPPO_EINVAL, "null argument");
+  const Cfg &c = env_cfg(env);
+#define HAS_FUSED(V_, NC_, NAV_, NP_) \
+  if (has_step_fused<V_, NC_, NAV_, NP_>(c)) return 1;
+  MHPPO_REG_SHAPES(HAS_FUSED)
+#undef HAS_FUSED
+  return 0;
+}
+
+int mhppo_rollout_step_fused(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
+                             const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
+  if (!env || !actor_cross || !actor_wait || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
+  if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
+    return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
+  if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
+  GUARD_DEVICE(env_device(env));
+  const Cfg &c = env_cfg(env);
+  if ((size_t)c.N * c.nS * c.P > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
+  if (bufs->feat_c != bufs->obs_c + (size_t)t * c.N * c.nS * NF_C)
+    return set_error(MHPPO_EINVAL, "fused step: feat_c must point at obs_c[t]");
+#define STEP_FUSED(V_, NC_, NAV_, NP_)                                                                           \
+  if (launch_step_fused<V_, NC_, NAV_, NP_>(c, env_bufs(env), *actor_cross, *actor_wait, eps, t, *bufs,          \
+                                            (hipStream_t)stream)) {                                              \
+    CHECK_HIP(hipGetLastError());                                                                                \
+    return MHPPO_OK;                                                                                             \
+  }
+  MHPPO_REG_SHAPES(STEP_FUSED)
+#undef STEP_FUSED
+  return set_error(MHPPO_EINVAL, "no fused step kernel for this shape (mhppo_rollout_fused_supported)");
 }
 
 int mhppo_rollout_check(mhppo_rollout_bufs *bufs, void *stream) {

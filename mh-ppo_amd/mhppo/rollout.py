@@ -47,8 +47,17 @@ def default_parts(n_envs, valu_policy=False):
     return 2 if (not valu_policy and n_envs >= 2 * PART_MIN_ENVS) else 1
 
 
+def default_fused():
+    """Off unless MHPPO_ROLLOUT_FUSED=1: the one-launch step (mhppo_rollout_step_fused) is
+    bit-identical but measured slower than the two-stream parts (config 3: 71 us per fused launch
+    against 64 us per two-part step, profiles/r04_fused/): at one wave per SIMD (the env step's
+    315 registers) its actors' MFMA chains and the env step run back to back in each wave."""
+    import os
+    return os.environ.get("MHPPO_ROLLOUT_FUSED", "0") == "1"
+
+
 class RolloutGPU:
-    def __init__(self, venv, T=None, valu_policy=False, parts=None):
+    def __init__(self, venv, T=None, valu_policy=False, parts=None, fused=None):
         if venv.variant == "4cars2":
             raise ValueError("4cars2 is an env-level variant only: the reference has no driver for it and its "
                              "PPO-driven followers earn no reward (Env_hybrid_multi_coop_4cars2.py:836-847)")
@@ -77,6 +86,9 @@ class RolloutGPU:
         self.exist = z((N, S), torch.uint8)
         self.eps = z((self.T, N, S), f32)
         self.u = z((N, S, P), f32)
+        # the fused one-launch step (one pedestrian, compiled shapes): bit-identical to the two launches
+        self.fused_ok = bool(_lib.lib().mhppo_rollout_fused_supported(venv.handle) == 1) and not valu_policy
+        self.fused = self.fused_ok and (default_fused() if fused is None else bool(fused))
         self.parts = default_parts(N, valu_policy) if parts is None else int(parts)
         if self.parts > 1 and valu_policy:
             raise ValueError("parts > 1 runs the MFMA policy kernel only")
@@ -152,13 +164,16 @@ class RolloutGPU:
                                             self.eps[0].numel(), st))
 
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
-                eps_tape=None, step_events=None, parts=None):
+                eps_tape=None, step_events=None, parts=None, fused=None):
         """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
-        replay recorded draws (parity mode); otherwise Philox noise is drawn.  parts: 1 forces the
-        one-chain loop for this call (default: self.parts); step_events implies it."""
+        replay recorded draws (parity mode); otherwise Philox noise is drawn.  fused: the one-launch
+        step (default: self.fused; needs self.fused_ok).  Unfused, parts: 1 forces the one-chain
+        loop for this call (default: self.parts); step_events implies it.  step_events brackets
+        each step's env-step launch (the fused launch when fused)."""
         L = _lib.lib()
+        fused = self.fused if fused is None else (bool(fused) and self.fused_ok)
         nparts = self.parts if parts is None else min(int(parts), self.parts)
-        if step_events is not None:
+        if step_events is not None or fused:
             nparts = 1
         self._bufs.parts = nparts
         if forced_choice is None or eps_tape is None:
@@ -175,7 +190,16 @@ class RolloutGPU:
         st = _lib.stream_ptr(device=dev)
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
-        if nparts > 1:
+        if fused:
+            for t in range(self.T):
+                self._bufs.feat_c = self.obs_c[t].data_ptr()  # features straight into the step's record
+                if step_events is not None:
+                    step_events[t][0].record()
+                _lib.check(L.mhppo_rollout_step_fused(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                                      _lib.ptr(self.eps[t]), t, ctypes.byref(self._bufs), st))
+                if step_events is not None:
+                    step_events[t][1].record()
+        elif nparts > 1:
             # Two-stream rollout: the parts' step chains (policy -> env step -> policy ...) are
             # independent, so one part's policy MFMA work fills the CUs that another part's
             # latency-bound env step leaves idle (one wave per SIMD, the launch lasting as long as

@@ -170,7 +170,7 @@ def test_two_part_rollout_equals_one_chain(case):
     outs = []
     for parts in (1, 2):
         venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=900)
-        ro = RolloutGPU(venv, parts=parts)
+        ro = RolloutGPU(venv, parts=parts, fused=False)
         torch.manual_seed(3)
         ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
         aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
@@ -182,3 +182,41 @@ def test_two_part_rollout_equals_one_chain(case):
         outs[-1]["state"] = venv.state_dict()["blob"]
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2, 300), ("coop", 2, 1, 2, 1000), ("scalable", 8, 1, 4, 257),
+                                  ("stop", 2, 1, 2, 130), ("4cars", 4, 1, 2, 8192)])
+def test_fused_step_equals_two_launches(case):
+    """mhppo_rollout_step_fused (RolloutGPU(fused=True): the actors' forward on f32 MFMA inside the
+    env-step launch, rows compacted by head per wave) gives bit-identical records, policy outputs
+    and env state to the policy + sample_env launches — ragged N (a partial last wave) included."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    v, nc, npd, nl, N = case
+    outs = []
+    for fused in (False, True):
+        venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=321)
+        ro = RolloutGPU(venv, parts=1, fused=fused)
+        assert ro.fused_ok and ro.fused == fused
+        torch.manual_seed(8)
+        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        ad = Model_PPO(ro.dc, 2, 2).cuda()
+        b = ro.collect(ac, aw, ad, seed=4, iteration=2)
+        torch.cuda.synchronize()
+        outs.append({k: getattr(b, k).clone() for k in ("a_d", "closest", "exist", "obs_c", "act", "logp", "rew",
+                                                         "ep_min", "feat_d", "logp_d")})
+        outs[-1]["out_c"] = ro.out_c.clone()
+        outs[-1]["state"] = venv.state_dict()["blob"]
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_fused_supported_shapes():
+    """mhppo_rollout_fused_supported: 1 for the one-pedestrian register-view shapes, 0 otherwise
+    (P = 2 runs the two launches)."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.rollout import RolloutGPU
+    assert RolloutGPU(VecCrosswalk("4cars", 64, 4, 1, 2)).fused_ok
+    assert not RolloutGPU(VecCrosswalk("coop", 64, 2, 2, 2)).fused_ok
