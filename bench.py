@@ -227,7 +227,7 @@ def main():
     env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
     step_us, fused_kern_us = {}, None
     modes = [("one_chain", 1, False)] + ([("parts", gpu.parts, False)] if gpu.parts > 1 else []) + \
-        ([("fused", 1, True)] if gpu.fused_ok else [])
+        ([("fused", 1, True)] if gpu.fused_ok else []) + [("product", None, None)]
     with torch.no_grad():
         for name, parts, fused in modes:
             algo.rollout.reset()
@@ -237,7 +237,7 @@ def main():
                 _lib.check(L.mhppo_kernel_timing_begin(T))
             e0.record()
             gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=7, iteration=0,
-                        parts=parts, fused=fused)
+                        parts=parts, fused=fused, graph=None if name == "product" else False)
             e1.record()
             torch.cuda.synchronize()
             if timed:
@@ -297,11 +297,13 @@ def main():
                          "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3),
                          "measured_on": "one extra 80-step rollout after the timed region, all N envs per launch"},
         "rollout_step_us": {**step_us, "parts_n": gpu.parts, "fused_kernel": fused_kern_us,
-                            "product": step_us["fused" if gpu.fused else ("parts" if gpu.parts > 1 else "one_chain")],
+                            "product_path": ("fused" if gpu.fused else ("parts" if gpu.parts > 1 else "one_chain")) +
+                            (" (HIP graph)" if gpu.use_graph and gpu.parts == 1 else ""),
                             "note": "wall time per rollout step, torch events around a whole 80-step collect: "
                                     "one_chain = policy + env-step launches, parts = those on two streams "
                                     "(env halves), fused = one launch per step (mhppo_rollout_step_fused; "
-                                    "fused_kernel = its dispatch-attached kernel time)"},
+                                    "fused_kernel = its dispatch-attached kernel time), product = the "
+                                    "product's collect (one_chain loops replay a captured HIP graph)"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)

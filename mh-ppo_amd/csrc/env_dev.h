@@ -292,6 +292,15 @@ struct RngT {
       double u2 = 1.0 - random();
       z = NV_MAGICCONST * (u1 - 0.5) / u2;
       double zz = z * z / 4.0;
+      // Squeeze around CPython's test zz <= -log(u2) (same decisions, same draws): with
+      // r = 1 - u2 (exact: the second random()), r < -log(u2) < r / u2, and for r >= 2^-40
+      // both gaps are >= r^2 / 2, i.e. >= 2^-41 relative — far beyond the roundings of r / u2
+      // and of log — so zz <= r accepts and zz > r / u2 rejects without the log.
+      const double r = 1.0 - u2;
+      if (r >= 0x1p-40) {
+        if (zz <= r) break;
+        if (zz > r / u2) continue;
+      }
       if (zz <= -log(u2)) break;
     }
     return mu + z * sigma;

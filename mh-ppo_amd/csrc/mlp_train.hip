@@ -1596,19 +1596,34 @@ __device__ __forceinline__ void load_sync_g(float *slot, const float *X, int nin
 // last tile loads synchronously.  body(slot, row0, nrows) runs each tile.  (Two tiles ahead in a
 // three-slot ring measured no faster: 1.764 / 1.867-1.871 ms vs 1.749-1.776 / 1.869-1.871 ms per
 // critic / actor launch, profiles/r04_x3_probe/ab_pf2.txt.)
+template <int KIND, class G>
+__device__ __forceinline__ void prefetch_any(const WaveSlot<G> &ws, float *slot, int64_t row0, const float *X, int nin,
+                                             const float *ret, const float *V, const float *act, const float *lp_old) {
+  if constexpr (G::NIC == NIN_CONT) prefetch_tile<KIND, LY>(slot, X, ret, V, act, lp_old, row0, ws.l);
+  else prefetch_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, ws.l);
+}
+// The first tile's LDS-DMA, issued by the kernel before it stages the weights (its own slot is
+// disjoint from the weight images), so the HBM latency of the first inputs overlaps the staging;
+// tile_loop(..., first_issued = true) then skips it.
+template <int KIND, class G>
+__device__ __forceinline__ void prefetch_first(const WaveSlot<G> &ws, int64_t gw, int64_t M, const float *X, int nin,
+                                               const float *ret, const float *V, const float *act,
+                                               const float *lp_old) {
+  if (gw < uniform_i64(M / 32)) prefetch_any<KIND, G>(ws, ws.inb, gw * 32, X, nin, ret, V, act, lp_old);
+}
+
 template <int KIND, class G, class Body>
 __device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int64_t nw, int64_t M, const float *X,
                                           int nin, const float *ret, const float *V, const float *act,
-                                          const float *lp_old, Body &&body) {
+                                          const float *lp_old, Body &&body, bool first_issued = false) {
   const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
   constexpr bool FIXED = G::NIC == NIN_CONT;  // the 13-input heads: the f32 path's slot loaders
   auto prefetch = [&](float *slot, int64_t row0) {
-    if constexpr (FIXED) prefetch_tile<KIND, LY>(slot, X, ret, V, act, lp_old, row0, ws.l);
-    else prefetch_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, ws.l);
+    prefetch_any<KIND, G>(ws, slot, row0, X, nin, ret, V, act, lp_old);
   };
   int cb = 0;
   MHPPO_MARK(0);
-  if (gw < nfull) prefetch(ws.inb, gw * 32);
+  if (gw < nfull && !first_issued) prefetch(ws.inb, gw * 32);
   for (int64_t tile = gw; tile < ntiles; tile += nw, cb ^= 1) {
     const int64_t row0 = tile * 32;
     const int nrows = (int)min((int64_t)32, M - row0);
@@ -1662,9 +1677,11 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   char *L8 = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const WaveSlot<G> ws(L8 + G::NET_B, w, l);
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+  prefetch_first<KIND, G>(ws, gw, M, X, nin, ret, V, act, lp_old);
   stage_net<G>(W, L8, tid, nin);
   __syncthreads();
-  const WaveSlot<G> ws(L8 + G::NET_B, w, l);
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
   Pass<KIND, KIND == K_CRITIC && G::NIC == NIN_CONT, true, G> p;
@@ -1672,10 +1689,12 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   float meanf = 0.f, stdf = 1.f;
   if (KIND != K_CRITIC) adv_norm(stats, m_global, meanf, stdf);
   const double inv_m = uniform_d(1.0 / m_global);
-  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  tile_loop<KIND, G>(ws, gw, nw, M, X, nin, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
-    p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
-  });
+  tile_loop<KIND, G>(
+      ws, gw, nw, M, X, nin, ret, V, act, lp_old,
+      [&](const float *slot, int64_t row0, int nrows) {
+        p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
+      },
+      true);
   const int np = Packed(geo_nin<G>(nin), G::NOUT).NP;
   fold_partials<G>(p, ws, L8, w, tid, np, gpart + (size_t)blockIdx.x * np, dpart + blockIdx.x * 3);
 }
@@ -1703,10 +1722,12 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   using G = G13;
+  const WaveSlot<G> ws(L8 + 2 * G::NET_B, w, l);
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
+  prefetch_first<K_CONT, G>(ws, gw, M, X, NIN_CONT, ret, V, act, lp_old);
   stage_net<G>(Wa, L8, tid, NIN_CONT);
   stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
-  const WaveSlot<G> ws(L8 + 2 * G::NET_B, w, l);
   Pass<K_CONT, false, PAIR_HB, G> pa;
   Pass<K_CRITIC, false, PAIR_HB, G> pc;
   pa.init(L8, ws);
@@ -1714,11 +1735,13 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   float meanf, stdf;
   adv_norm(stats, m_global, meanf, stdf);
   const double inv_m = uniform_d(1.0 / m_global);
-  const int64_t gw = (int64_t)blockIdx.x * WAVES + w, nw = (int64_t)gridDim.x * WAVES;
-  tile_loop<K_CONT, G>(ws, gw, nw, M, X, NIN_CONT, ret, V, act, lp_old, [&](const float *slot, int64_t row0, int nrows) {
-    pa.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
-    pc.tile(ws, slot, row0, nrows, V, 0.f, 1.f, inv_m, out_mean, out_std);
-  });
+  tile_loop<K_CONT, G>(
+      ws, gw, nw, M, X, NIN_CONT, ret, V, act, lp_old,
+      [&](const float *slot, int64_t row0, int nrows) {
+        pa.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
+        pc.tile(ws, slot, row0, nrows, V, 0.f, 1.f, inv_m, out_mean, out_std);
+      },
+      true);
   constexpr int NWP = Packed(NIN_CONT, 1).NP;
   const int64_t nb = gridDim.x, b = blockIdx.x;
   fold_partials<G>(pa, ws, L8, w, tid, NWP, gpart + (size_t)b * NWP, dpart + b * 3);
@@ -1754,6 +1777,43 @@ __global__ void __launch_bounds__(256)
     return;
   }
   tmp[(size_t)g * nd + k] = s;
+}
+
+// The split kernels' block partials (at most one per CU: nb <= 1024) in ONE launch: a 1 024-thread
+// block per 64 gradient slots; thread (g, c) sums partials [g nb / 16, (g + 1) nb / 16) of slot c
+// in order (16 coalesced rows per load step), then thread (0, c) adds the 16 group sums in order.
+// blockIdx.y = net (the pair launch).  Fixed order: deterministic.
+constexpr int RD_COLS = 64, RD_GROUPS = 16;
+__global__ void __launch_bounds__(RD_COLS * RD_GROUPS)
+    k_grad_reduce_blocks(const double *gpart, const double *dpart, int nb, int np, float *grad, double *out3,
+                         float *grad1, double *out3_1) {
+  __shared__ double red[RD_GROUPS][RD_COLS];
+  const int c = blockIdx.x * RD_COLS + (threadIdx.x & (RD_COLS - 1)), g = threadIdx.x / RD_COLS;
+  const int nd = np + 3;
+  if (blockIdx.y) {
+    gpart += (size_t)nb * np;
+    dpart += (size_t)nb * 3;
+    grad = grad1;
+    out3 = out3_1;
+  }
+  const int i0 = g * nb / RD_GROUPS, i1 = (g + 1) * nb / RD_GROUPS;
+  double s = 0.0;
+  if (c < np) {
+#pragma unroll 16
+    for (int i = i0; i < i1; i++) s += gpart[(size_t)i * np + c];
+  } else if (c < nd) {
+    for (int i = i0; i < i1; i++) s += dpart[(size_t)i * 3 + (c - np)];
+  }
+  red[g][threadIdx.x & (RD_COLS - 1)] = s;
+  __syncthreads();
+  if (g != 0 || c >= nd) return;
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < RD_GROUPS; q++) t += red[q][threadIdx.x];
+  if (c < np)
+    grad[c] = (float)t;
+  else if (out3)
+    out3[c - np] += t;
 }
 
 __global__ void __launch_bounds__(256)
@@ -1907,14 +1967,15 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   }
 #undef MLP_ARGS
   const int np = n_params(n_in, kind == K_CHOICE ? 2 : 1);
-  if (split || split_c)  // one float64 partial per block
-    hipLaunchKernelGGL(k_grad_stage1<double>, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s,
-                       reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, wk.t);
-  else  // one float partial per wave
+  if (split || split_c) {  // one float64 partial per block: one reduction launch
+    hipLaunchKernelGGL(k_grad_reduce_blocks, dim3((np + 3 + RD_COLS - 1) / RD_COLS), dim3(RD_COLS * RD_GROUPS), 0, s,
+                       reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, grad, sums, nullptr, nullptr);
+  } else {  // one float partial per wave: two stages
     hipLaunchKernelGGL(k_grad_stage1<float>, dim3((np + 3 + 255) / 256, RG), dim3(256), 0, s, wk.g, wk.d, nw, np,
                        wk.t);
-  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums, nullptr,
-                     nullptr);
+    hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256), dim3(256), 0, s, wk.t, np, grad, sums, nullptr,
+                       nullptr);
+  }
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }
@@ -1947,11 +2008,10 @@ extern "C" int mhppo_mlp_train_pair(const float *packed_actor, const float *pack
   hipLaunchKernelGGL(k_mlp_train_x3_pair, dim3((unsigned)blocks), dim3(64 * x3::WAVES), x3::G13::LDS_BYTES_PAIR, s,
                      packed_actor, packed_critic, X, M, ret, value, act, logp_old, stats, m_global, out_mean, out_std,
                      reinterpret_cast<double *>(wk.g), wk.d);
-  // the two nets' block partials (actor [0, blocks), critic [blocks, 2 blocks)) in one launch pair
-  hipLaunchKernelGGL(k_grad_stage1<double>, dim3((np + 3 + 255) / 256, RG, 2), dim3(256), 0, s,
-                     reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, wk.t);
-  hipLaunchKernelGGL(k_grad_stage2, dim3((np + 3 + 255) / 256, 1, 2), dim3(256), 0, s, wk.t, np, grad_actor,
-                     sums_actor, grad_critic, sums_critic);
+  // the two nets' block partials (actor [0, blocks), critic [blocks, 2 blocks)) in one launch
+  hipLaunchKernelGGL(k_grad_reduce_blocks, dim3((np + 3 + RD_COLS - 1) / RD_COLS, 2), dim3(RD_COLS * RD_GROUPS), 0, s,
+                     reinterpret_cast<const double *>(wk.g), wk.d, (int)blocks, np, grad_actor, sums_actor,
+                     grad_critic, sums_critic);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
 }

@@ -206,7 +206,9 @@ class Algo_PPO:
         dev = self.venv.device
         c, w, d = r.cross, r.wait, r.choice
         with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
-            counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
+            counts = d.get("counts")  # queued with the bucketing, before its host sync
+            if counts is None:
+                counts = torch.stack([(d["act"] == 0).sum(), (d["act"] == 1).sum()]).to(torch.float64)
             if ppo._dp():  # global row counts: one all-reduce and one host sync
                 loc = torch.cat([torch.tensor([c["ret"].numel(), w["ret"].numel(), d["ret"].numel()],
                                               dtype=torch.float64, device=dev), counts])

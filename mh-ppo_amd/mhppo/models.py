@@ -44,7 +44,11 @@ class Model_PPO(nn.Module):
     # read the weights and write the gradient in place (no per-launch cat / copy), and one
     # fused Adam launch updates a whole net.
     def _params(self):
-        return [p for lay in (self.layer1, self.layer2, self.layer3, self.layer4) for p in (lay.weight, lay.bias)]
+        # straight from the module / parameter dicts (nn.Module.__getattr__ costs ~1 us a lookup, and
+        # flat() / grad_flat() run once per head and update): always the current registrations
+        m = self._modules
+        return [q for lay in (m["layer1"], m["layer2"], m["layer3"], m["layer4"])
+                for q in (lay._parameters["weight"], lay._parameters["bias"])]
 
     def _flatten(self):
         ps = self._params()

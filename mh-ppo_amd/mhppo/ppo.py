@@ -351,6 +351,78 @@ def _use_pair(h):
     return PIPELINE_PAIRS if PIPELINE_PAIRS is not None else h.m <= PAIR_MAX_ROWS
 
 
+class _HeadPlan:
+    """One head's launch arguments for a whole train_epochs call, resolved once: the batch as
+    contiguous float32 (16-byte aligned rows), the nets' flat weight / gradient pointers (fixed
+    while the epochs run: the fused Adam updates them in place) and one V buffer.  Per pass only
+    the stats / sums pointers change — the Python cost of a pass is one ctypes call (the per-call
+    re-validation in k_mlp_train, ~60 us of host time, left the GPU idle on small batches)."""
+
+    def __init__(self, h):
+        for net, kind in ((h.critic, KIND_CRITIC), (h.actor, KIND_CONT if h.kind == "c" else KIND_CHOICE)):
+            want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
+            if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):
+                raise ValueError(f"fused kernel kind {kind} cannot train a model_type {net.model_type} "
+                                 f"{net.n_in}->{net.n_out} Model_PPO")
+        obs = h.obs.float().contiguous()
+        if obs.data_ptr() % 16:
+            obs = obs.clone()
+        self.obs, self.ret = obs, h.ret.float().contiguous()
+        self.M = obs.shape[0]
+        self.lp = h.logp.float().contiguous()
+        self.act = h.act.float().contiguous() if (h.kind == "c" or h.per_row) else None
+        self.counts = None if (h.kind == "c" or h.per_row) else h.counts
+        self.V = torch.empty(self.M, dtype=torch.float32, device=obs.device)
+        self.n_in = h.actor.n_in
+        self.wa, self.wc = h.actor.flat().data_ptr(), h.critic.flat().data_ptr()
+        self.ga, self.gc = h.actor.grad_flat().data_ptr(), h.critic.grad_flat().data_ptr()
+        self.mean, self.std = float(h.actor.mean), float(h.actor.std)
+        self.flags = TRAIN_EXACT_F32 if h.exact else 0
+        self.akind = KIND_CONT if h.kind == "c" else KIND_CHOICE
+        self.keep = (h.actor.flat(), h.critic.flat())  # the storages the pointers above point into
+
+
+def _ev_begin():
+    if TRAIN_EVENTS is None:
+        return None
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev[0].record()
+    return ev
+
+
+def _ev_end(ev, kind, n_in, M):
+    if ev is not None:
+        ev[1].record()
+        TRAIN_EVENTS.append((kind, n_in, M, ev[0], ev[1]))
+
+
+# The three launch helpers of train_epochs (module-level so CPU test doubles can stand in for them:
+# tests/test_dp_gloo.py).  sums / stats are float64 views: [3] rows of the step's sums, [2] stats.
+def _critic_pass(p, h, sums, st):
+    ev = _ev_begin()
+    _lib.check(_lib.lib().mhppo_mlp_train(
+        KIND_CRITIC | p.flags, p.n_in, p.wc, p.obs.data_ptr(), p.M, p.ret.data_ptr(), p.V.data_ptr(), None, None, None,
+        None, h.m, 0.0, 1.0, p.gc, sums.data_ptr(), st))
+    _ev_end(ev, KIND_CRITIC, p.n_in, p.M)
+
+
+def _actor_pass(p, h, stats, sums, st):
+    ev = _ev_begin()
+    _lib.check(_lib.lib().mhppo_mlp_train(
+        p.akind | p.flags, p.n_in, p.wa, p.obs.data_ptr(), p.M, p.ret.data_ptr(), p.V.data_ptr(),
+        None if p.act is None else p.act.data_ptr(), p.lp.data_ptr(), stats.data_ptr(),
+        None if p.counts is None else p.counts.data_ptr(), h.m, p.mean, p.std, p.ga, sums.data_ptr(), st))
+    _ev_end(ev, p.akind, p.n_in, p.M)
+
+
+def _pair_pass(p, h, stats, sums_a, sums_c, st):
+    ev = _ev_begin()
+    _lib.check(_lib.lib().mhppo_mlp_train_pair(
+        p.wa, p.wc, p.obs.data_ptr(), p.M, p.ret.data_ptr(), p.V.data_ptr(), p.act.data_ptr(), p.lp.data_ptr(),
+        stats.data_ptr(), h.m, p.mean, p.std, p.ga, sums_a.data_ptr(), p.gc, sums_c.data_ptr(), st))
+    _ev_end(ev, 3, 13, p.M)  # kind 3: a fused pair launch (two passes)
+
+
 def train_epochs(heads, n_epochs, bucket=None):
     """n_epochs full-batch epochs of every head, run as a pipeline of n_epochs + 1 steps: step k
     runs the actor passes of epoch k - 1 and the critic passes of epoch k (a continuous head on the
@@ -359,11 +431,14 @@ def train_epochs(heads, n_epochs, bucket=None):
     the Adam steps.  The same arithmetic as n_epochs calls of train_epoch: the actor of epoch e
     uses V_e and the advantage sums of the critic pass e (critic weights of epoch e), the critic
     of epoch e + 1 the critic's weights after its Adam step e; each optimiser steps n_epochs
-    times.  Returns this rank's (actor, critic) loss sums of the last epoch per head."""
+    times.  Returns this rank's (actor, critic) loss sums of the last epoch per head.
+    The launches go straight through the C-ABI with each head's arguments resolved once
+    (_HeadPlan); an empty head (M == 0) runs k_mlp_train's empty-shard path."""
     H = len(heads)
     dev = heads[0].obs.device
     paired = [_use_pair(h) for h in heads]
-    V = [None] * H      # V_e of each head (a paired head's buffer is updated in place)
+    plans = [_HeadPlan(h) if h.obs.shape[0] > 0 else None for h in heads]
+    st = _lib.stream_ptr().value if dev.type == "cuda" else None
     stats = None        # all-reduced advantage sums of the previous step's critic passes [2H]
     out = [[None, None] for _ in range(H)]
     for k in range(n_epochs + 1):
@@ -371,29 +446,35 @@ def train_epochs(heads, n_epochs, bucket=None):
         crit = k < n_epochs
         trained = []
         for i, h in enumerate(heads):
+            p = plans[i]
             sc, sa = sums[i], sums[H + i]
-            st = stats[2 * i:2 * i + 2] if k > 0 else None
+            stp = stats[2 * i:2 * i + 2] if k > 0 else None
+            if p is None:  # an empty shard: zero gradients, sums unchanged (k_mlp_train's M == 0 path)
+                if k > 0:
+                    cont = h.kind == "c"
+                    k_mlp_train(KIND_CONT if cont else KIND_CHOICE, h.actor, h.obs, h.ret, h.obs.new_empty(0),
+                                h.act if (cont or h.per_row) else None, h.logp, stp,
+                                None if (cont or h.per_row) else h.counts, m_global=h.m, sums=sa, exact=h.exact)
+                    trained.append(h.actor)
+                    out[i][0] = sums[H + i, 0:1]
+                if crit:
+                    k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sc, exact=h.exact)
+                    trained.append(h.critic)
+                    out[i][1] = sums[i, 0:1]
+                continue
             if k > 0 and crit and paired[i]:
-                k_mlp_train_pair(h.actor, h.critic, h.obs, h.ret, V[i], h.act, h.logp, st, h.m, sa, sc)
+                _pair_pass(p, h, stp, sa, sc, st)
                 trained += [h.actor, h.critic]
-                out[i] = [sa[0:1], sc[0:1]]
+                out[i] = [sums[H + i, 0:1], sums[i, 0:1]]
                 continue
             if k > 0:  # the actor pass of epoch k - 1
-                if h.kind == "c":
-                    k_mlp_train(KIND_CONT, h.actor, h.obs, h.ret, V[i], h.act, h.logp, st, m_global=h.m, sums=sa,
-                                exact=h.exact)
-                elif h.per_row:
-                    k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], h.act.float(), h.logp, st, None,
-                                m_global=h.m, sums=sa, exact=h.exact)
-                else:
-                    k_mlp_train(KIND_CHOICE, h.actor, h.obs, h.ret, V[i], None, h.logp, st, h.counts, m_global=h.m,
-                                sums=sa, exact=h.exact)
+                _actor_pass(p, h, stp, sa, st)
                 trained.append(h.actor)
-                out[i][0] = sa[0:1]
+                out[i][0] = sums[H + i, 0:1]
             if crit:  # the critic pass of epoch k
-                _, _, V[i] = k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sc, exact=h.exact)
+                _critic_pass(p, h, sc, st)
                 trained.append(h.critic)
-                out[i][1] = sc[0:1]
+                out[i][1] = sums[i, 0:1]
         if crit:
             stats = sums[:H, 1:3].reshape(-1).contiguous()
             _allreduce_(stats)
@@ -403,6 +484,7 @@ def train_epochs(heads, n_epochs, bucket=None):
             _allreduce_net_grads(*trained)
         adam_steps([h.opt_actor for h in heads if h.actor in trained] +
                    [h.opt_critic for h in heads if h.critic in trained])
+    del plans
     return [tuple(o) for o in out]
 
 

@@ -47,6 +47,13 @@ def default_parts(n_envs, valu_policy=False):
     return 2 if (not valu_policy and n_envs >= 2 * PART_MIN_ENVS) else 1
 
 
+def default_graph():
+    """Replay the one-chain step loop from a captured HIP graph (RolloutGPU.collect) unless
+    MHPPO_ROLLOUT_GRAPH=0 (A/B)."""
+    import os
+    return os.environ.get("MHPPO_ROLLOUT_GRAPH", "1") != "0"
+
+
 def default_fused():
     """Off unless MHPPO_ROLLOUT_FUSED=1: the one-launch step (mhppo_rollout_step_fused) is
     bit-identical but measured slower than the two-stream parts (config 3: 71 us per fused launch
@@ -104,6 +111,9 @@ class RolloutGPU:
         b.flags = 1 if valu_policy else 0  # MHPPO_ROLLOUT_VALU_POLICY
         b.parts = self.parts
         self._bufs = b
+        # captured one-chain step loops, keyed by what their launches bake in (collect)
+        self._graphs = {}
+        self.use_graph = dev.type == "cuda" and default_graph()
         # parts > 1: part p > 0 steps on its own stream (created once), part 0 on the caller's
         self._side = [torch.cuda.Stream(device=dev) for _ in range(self.parts - 1)] if dev.type == "cuda" else []
 
@@ -163,13 +173,35 @@ class RolloutGPU:
         _lib.check(L.mhppo_philox_normal_2d(key, _CTR_STEP + off * self.S, _CTR_STEP, _lib.ptr(self.eps), self.T,
                                             self.eps[0].numel(), st))
 
+    def _step_loop(self, L, mx, mw, fused, st, step_events):
+        """The T steps as one chain on stream `st`: the fused launch, or policy + env step."""
+        for t in range(self.T):
+            if self.P == 1:  # features straight into the step's record (include/mhppo.h)
+                self._bufs.feat_c = self.obs_c[t].data_ptr()
+            if fused:
+                if step_events is not None:
+                    step_events[t][0].record()
+                _lib.check(L.mhppo_rollout_step_fused(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                                      _lib.ptr(self.eps[t]), t, ctypes.byref(self._bufs), st))
+            else:
+                _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                                  ctypes.byref(self._bufs), st))
+                if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
+                    step_events[t][0].record()
+                _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
+                                                      ctypes.byref(self._bufs), st))
+            if step_events is not None:
+                step_events[t][1].record()
+
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
-                eps_tape=None, step_events=None, parts=None, fused=None):
+                eps_tape=None, step_events=None, parts=None, fused=None, graph=None):
         """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
         replay recorded draws (parity mode); otherwise Philox noise is drawn.  fused: the one-launch
         step (default: self.fused; needs self.fused_ok).  Unfused, parts: 1 forces the one-chain
         loop for this call (default: self.parts); step_events implies it.  step_events brackets
-        each step's env-step launch (the fused launch when fused)."""
+        each step's env-step launch (the fused launch when fused).  graph: replay the one-chain loop
+        from a captured HIP graph (default: self.use_graph; pass False while mhppo_kernel_timing is
+        on — graph nodes carry no timing events)."""
         L = _lib.lib()
         fused = self.fused if fused is None else (bool(fused) and self.fused_ok)
         nparts = self.parts if parts is None else min(int(parts), self.parts)
@@ -190,16 +222,25 @@ class RolloutGPU:
         st = _lib.stream_ptr(device=dev)
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
-        if fused:
-            for t in range(self.T):
-                self._bufs.feat_c = self.obs_c[t].data_ptr()  # features straight into the step's record
-                if step_events is not None:
-                    step_events[t][0].record()
-                _lib.check(L.mhppo_rollout_step_fused(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
-                                                      _lib.ptr(self.eps[t]), t, ctypes.byref(self._bufs), st))
-                if step_events is not None:
-                    step_events[t][1].record()
-        elif nparts > 1:
+        graph = self.use_graph if graph is None else (bool(graph) and dev.type == "cuda")
+        if nparts == 1 and step_events is None and graph:
+            # The one-chain loop's 80 (fused) or 160 launches as one captured HIP graph, replayed:
+            # the same kernels and arguments (the pointers, step indices and the actors' mean / std
+            # are baked into the graph's nodes and key it), without the per-launch host work that
+            # leaves small-N steps launch-bound.
+            key = (fused, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
+            g = self._graphs.get(key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._step_loop(L, mx, mw, fused, _lib.stream_ptr(device=dev), None)
+                if len(self._graphs) > 8:
+                    self._graphs.clear()
+                self._graphs[key] = g
+            g.replay()
+        elif fused or nparts == 1:
+            self._step_loop(L, mx, mw, fused, st, step_events)
+        else:
             # Two-stream rollout: the parts' step chains (policy -> env step -> policy ...) are
             # independent, so one part's policy MFMA work fills the CUs that another part's
             # latency-bound env step leaves idle (one wave per SIMD, the launch lasting as long as
@@ -220,18 +261,6 @@ class RolloutGPU:
                                                                ctypes.byref(self._bufs), part, sp))
             for side in self._side[:nparts - 1]:
                 main.wait_stream(side)
-        else:
-            for t in range(self.T):
-                if self.P == 1:  # features straight into the step's record (include/mhppo.h)
-                    self._bufs.feat_c = self.obs_c[t].data_ptr()
-                _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
-                                                  ctypes.byref(self._bufs), st))
-                if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
-                    step_events[t][0].record()
-                _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
-                                                      ctypes.byref(self._bufs), st))
-                if step_events is not None:
-                    step_events[t][1].record()
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
         # obs_c/act/logp/rew: [N, S, T(, 13)] views of the time-major buffers (*_tm)
         return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,
@@ -302,7 +331,33 @@ def bucket_segments(batch, fix_bucket=False, status=None):
     exist = batch.exist.bool().reshape(-1)
     cross = exist & (action_d_i <= 0).reshape(-1)
     wait = exist & (action_d_i > 0).reshape(-1)
-    sizes = [cross.sum(), wait.sum(), exist.sum()]
+    NS = N * S
+    # Everything is queued before the one host sync, so the GPU runs it while the host waits for
+    # the sizes: the returns scan; each segment's bucket position (its rank among its bucket's
+    # segments in (env, slot) order = the nonzero order); the bucket scatter into buffers with
+    # room for every segment; the choice batch gathered over all segment slots (existing ones
+    # first: nonzero_static pads with slot 0); the choice action counts.  After the sync the
+    # batches are leading views of those buffers.
+    ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
+    cc, cw = torch.cumsum(cross, 0), torch.cumsum(wait, 0)
+    pos = torch.where(cross, cc - 1, torch.where(wait, cw - 1, -1))
+    bucket = wait.to(torch.int8)
+    cross_r, wait_r = scatter_positions(pos, bucket, (NS, NS), NS, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm,
+                                        ret, batch.rew_tm)
+    seg_all = torch.nonzero_static(exist, size=NS, fill_value=0).squeeze(1)
+    cl = batch.closest.reshape(NS).long().index_select(0, seg_all)
+    base = seg_all * P + cl
+    dc = batch.feat_d.shape[-1]
+    a_sel = batch.a_d.reshape(-1).index_select(0, base)
+    choice = dict(
+        obs=batch.feat_d.reshape(NS * P, dc).index_select(0, base),
+        act=a_sel,
+        logp=batch.logp_d.reshape(-1).index_select(0, base),
+        ret=batch.ep_min.reshape(-1).index_select(0, seg_all).float(),
+    )
+    a_car = batch.a_d.reshape(NS, P).gather(1, batch.closest.reshape(NS, 1).long()).reshape(-1)
+    counts = torch.stack([(exist & (a_car == 0)).sum(), (exist & (a_car == 1)).sum()]).to(torch.float64)
+    sizes = [cc[-1], cw[-1], exist.sum()]
     if status is not None:
         sizes.append(status.reshape(-1)[0].to(torch.int64))
     sizes = torch.stack(sizes).tolist()
@@ -311,24 +366,13 @@ def bucket_segments(batch, fix_bucket=False, status=None):
             status.zero_()
         raise_if_nan_status(sizes[3])
     n_cross, n_wait, n_all = sizes[:3]
-    seg_cross = torch.nonzero_static(cross, size=n_cross).squeeze(1)
-    seg_wait = torch.nonzero_static(wait, size=n_wait).squeeze(1)
-    seg_all = torch.nonzero_static(exist, size=n_all).squeeze(1)
-    ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
-
-    cross_r, wait_r = scatter_buckets(seg_cross, seg_wait, N * S, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm,
-                                      ret, batch.rew_tm)
-
-    cl = batch.closest.reshape(N * S).long().index_select(0, seg_all)
-    base = seg_all * P + cl
-    dc = batch.feat_d.shape[-1]
-    choice = dict(
-        obs=batch.feat_d.reshape(N * S * P, dc).index_select(0, base),
-        act=batch.a_d.reshape(-1).index_select(0, base),
-        logp=batch.logp_d.reshape(-1).index_select(0, base),
-        ret=batch.ep_min.reshape(-1).index_select(0, seg_all).float(),
-        n_seg=n_all,
-    )
+    for o, n in ((cross_r, n_cross), (wait_r, n_wait)):
+        for k in ("obs", "act", "logp", "ret", "rew"):
+            o[k] = o[k][:n * T]
+        o["n_seg"] = n
+    choice = {k: v[:n_all] for k, v in choice.items()}
+    choice["n_seg"] = n_all
+    choice["counts"] = counts  # float64 [2] on the device: (act == 0).sum(), (act == 1).sum()
     return cross_r, wait_r, choice
 
 
@@ -338,11 +382,19 @@ def scatter_buckets(seg0, seg1, NS, T, obs_tm, act_tm, logp_tm, ret_tm, rew_tm):
     dev = obs_tm.device
     pos = torch.full((NS,), -1, dtype=torch.int64, device=dev)
     bucket = torch.zeros(NS, dtype=torch.int8, device=dev)
-    outs, dst = [], (_lib.BucketDst * 2)()
     for b, seg in enumerate((seg0, seg1)):
-        n = int(seg.numel())
-        pos[seg] = torch.arange(n, dtype=torch.int64, device=dev)
+        pos[seg] = torch.arange(int(seg.numel()), dtype=torch.int64, device=dev)
         bucket[seg] = b
+    return scatter_positions(pos, bucket, (int(seg0.numel()), int(seg1.numel())), NS, T, obs_tm, act_tm, logp_tm,
+                             ret_tm, rew_tm)
+
+
+def scatter_positions(pos, bucket, sizes, NS, T, obs_tm, act_tm, logp_tm, ret_tm, rew_tm):
+    """scatter_buckets with the segments given as positions: segment s goes to row block pos[s]
+    of bucket bucket[s] (pos < 0: no bucket); sizes = the two buckets' segment counts."""
+    dev = obs_tm.device
+    outs, dst = [], (_lib.BucketDst * 2)()
+    for b, n in enumerate(sizes):
         o = dict(obs=torch.empty(n * T, NF_C, dtype=torch.float32, device=dev),
                  act=torch.empty(n * T, dtype=torch.float32, device=dev),
                  logp=torch.empty(n * T, dtype=torch.float32, device=dev),

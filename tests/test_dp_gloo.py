@@ -102,6 +102,18 @@ def _install_cpu_doubles(ppo):
     ppo.k_mlp_train = mlp_train
     ppo.k_mlp_train_pair = mlp_train_pair
 
+    # train_epochs' launch helpers (ppo._HeadPlan arguments) on the same doubles
+    def critic_pass(p, h, sums, st):
+        p.V.copy_(mlp_train(0, h.critic, p.obs, p.ret, m_global=h.m, sums=sums)[2])
+
+    def actor_pass(p, h, stats, sums, st):
+        mlp_train(p.akind, h.actor, p.obs, p.ret, p.V, p.act, p.lp, stats, p.counts, m_global=h.m, sums=sums)
+
+    def pair_pass(p, h, stats, sums_a, sums_c, st):
+        mlp_train_pair(h.actor, h.critic, p.obs, p.ret, p.V, p.act, p.lp, stats, h.m, sums_a, sums_c)
+
+    ppo._critic_pass, ppo._actor_pass, ppo._pair_pass = critic_pass, actor_pass, pair_pass
+
 
 def _run(rank, world, port, data, out_q):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]

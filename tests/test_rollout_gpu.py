@@ -147,7 +147,7 @@ def test_kernel_timing_events_leave_results_unchanged():
         ad = Model_PPO(ro.dc, 2, 2).cuda()
         if timed:
             _lib.check(L.mhppo_kernel_timing_begin(50))  # fewer than the episode's 80 steps
-        outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=3, iteration=0)))
+        outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=3, iteration=0, graph=False)))
         if timed:
             ms, n = ctypes.c_double(0.0), ctypes.c_int32(0)
             _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(ms), ctypes.byref(n)))
@@ -220,3 +220,38 @@ def test_fused_supported_shapes():
     from mhppo.rollout import RolloutGPU
     assert RolloutGPU(VecCrosswalk("4cars", 64, 4, 1, 2)).fused_ok
     assert not RolloutGPU(VecCrosswalk("coop", 64, 2, 2, 2)).fused_ok
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_graph_replay_equals_eager(fused):
+    """RolloutGPU.collect(graph=True): the one-chain step loop captured once as a HIP graph and
+    replayed gives bit-identical records and env state to the eager launches — over two
+    iterations with new noise and with the actors' weights changed in place in between (the graph
+    reads the live weights), and a new graph for other actor objects."""
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import RolloutGPU
+    outs = []
+    for graph in (False, True):
+        venv = VecCrosswalk("coop", 1000, 2, 1, 2, seed_base=77)
+        ro = RolloutGPU(venv, parts=1, fused=fused)
+        torch.manual_seed(9)
+        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+        ad = Model_PPO(ro.dc, 2, 2).cuda()
+        rec = []
+        for it in range(3):
+            if it == 2:
+                with torch.no_grad():
+                    ac.flat().mul_(0.9)
+                    aw.flat().add_(0.01)
+            b = ro.collect(ac, aw, ad, seed=5, iteration=it, graph=graph)
+            torch.cuda.synchronize()
+            rec.append({k: getattr(b, k).clone() for k in ("a_d", "obs_c", "act", "logp", "rew", "ep_min")})
+            rec[-1]["state"] = venv.state_dict()["blob"]
+            venv.reset(want_obs=False)
+        assert len(ro._graphs) == (1 if graph else 0)
+        outs.append(rec)
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

@@ -18,7 +18,36 @@ ap.add_argument("--exact", action="store_true", help="the exact f32-MFMA kernel 
 ap.add_argument("--pair", action="store_true", help="also time the fused actor+critic launch (mhppo_mlp_train_pair)")
 ap.add_argument("--choice", type=int, default=0, help="also time a choice head with this many inputs, split vs exact")
 ap.add_argument("--choice-rows", type=int, default=655360)
+ap.add_argument("--sweep", action="store_true",
+                help="per-launch time of critic / actor passes at 1, 2, 4 ... 64 tiles per wave (kernel only, "
+                     "HIP events around the x3 launch are not separable: reported per k_mlp_train call)")
 a = ap.parse_args()
+if a.sweep:
+    torch.manual_seed(0)
+    act_ = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
+    cri_ = Model_PPO(13, 1, 0).cuda()
+    for tpw in (1, 2, 4, 8, 16, 32, 64):
+        Ms = 32 * 1024 * tpw
+        xo = torch.randn(Ms, 13, device="cuda") * 3
+        xr = torch.randn(Ms, device="cuda") * 8 - 20
+        xa = torch.randn(Ms, device="cuda") - 1
+        xl = torch.randn(Ms, device="cuda") * 0.3 - 0.9
+        res = []
+        for kind in (0, 1):
+            ppo.TRAIN_EVENTS = []
+            for r in range(a.reps + 2):
+                if r == 2:
+                    torch.cuda.synchronize()
+                    ppo.TRAIN_EVENTS = []
+                if kind == 0:
+                    _, sc_, V_ = ppo.k_mlp_train(0, cri_, xo, xr, m_global=float(Ms))
+                else:
+                    ppo.k_mlp_train(1, act_, xo, xr, V_, xa, xl, sc_[1:3].clone(), m_global=float(Ms))
+            torch.cuda.synchronize()
+            res.append(sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in ppo.TRAIN_EVENTS) / a.reps * 1e3)
+        print(f"tiles/wave {tpw:3d} rows {Ms:8d}: critic {res[0]:8.1f} us  actor {res[1]:8.1f} us", flush=True)
+    ppo.TRAIN_EVENTS = None
+    sys.exit(0)
 M = a.rows
 torch.manual_seed(0)
 actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()

@@ -32,7 +32,7 @@ with torch.no_grad():
         torch.cuda.synchronize()
         _lib.check(L.mhppo_kernel_timing_begin(T))
         algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
-                                 iteration=it)
+                                 iteration=it, parts=1, graph=False)
         buf = (ctypes.c_float * T)()
         n = ctypes.c_int32(0)
         _lib.check(L.mhppo_kernel_timing_end_each(buf, T, ctypes.byref(n)))
