@@ -84,8 +84,10 @@ def pmc_traffic(*patterns):
         ks = json.load(open(path))["kernels"]
     except (OSError, ValueError, KeyError):
         return None
+    # a pattern is a substring or a tuple of substrings that must all occur in the kernel's name
+    match = lambda k, p: all(q in k for q in p) if isinstance(p, tuple) else p in k  # noqa: E731
     vals = [v["hbm_bytes_per_launch"] for k, v in ks.items()
-            if any(p in k for p in patterns) and v.get("hbm_bytes_per_launch")]
+            if any(match(k, p) for p in patterns) and v.get("hbm_bytes_per_launch")]
     return sum(vals) / len(vals) if vals else None
 
 
@@ -264,7 +266,7 @@ def main():
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     split = not algo.exact_f32
     peak = X3_MFMA_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
-    traffic = (pmc_traffic("k_mlp_train_x3<0", "k_mlp_train_x3<1") if split else
+    traffic = (pmc_traffic(("k_mlp_train_x3<0", "Geo<16, 1, 13>"), ("k_mlp_train_x3<1", "Geo<16, 1, 13>")) if split else
                pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>"))
     traffic_env = pmc_traffic("k_sample_env")
     agents = "ragged 1-8 existing of 8 slots" if variant == "scalable" else S

@@ -6,6 +6,8 @@
 set -o pipefail
 OUT=gpurun_out/${1:-pmc}; CFG=${2:-3}; shift 2; EXTRA="$@"; mkdir -p $OUT
 export TMPDIR=/tmp
+# one-chain rollout: every env-step launch covers all N envs (the bench's env roofline is per full launch)
+export MHPPO_ROLLOUT_PARTS=1
 for c in FETCH_SIZE WRITE_SIZE; do
   d=$OUT/$(echo $c | tr A-Z a-z | cut -d_ -f1)
   timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $d -o run -- python3 bench.py --config $CFG $EXTRA --no-cpu-baseline --steps 1 --warmup 1 > $d.log 2>&1 || { echo "PMC $c FAILED"; tail -20 $d.log; exit 1; }
