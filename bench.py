@@ -300,12 +300,13 @@ def main():
                          "measured_on": "one extra 80-step rollout after the timed region, all N envs per launch"},
         "rollout_step_us": {**step_us, "parts_n": gpu.parts, "fused_kernel": fused_kern_us,
                             "product_path": ("fused" if gpu.fused else ("parts" if gpu.parts > 1 else "one_chain")) +
-                            (" (HIP graph)" if gpu.use_graph and gpu.parts == 1 else ""),
+                            (" (HIP graph)" if gpu.use_graph and (gpu.parts == 1 or gpu.fused or gpu.use_graph == 2)
+                             else ""),
                             "note": "wall time per rollout step, torch events around a whole 80-step collect: "
                                     "one_chain = policy + env-step launches, parts = those on two streams "
                                     "(env halves), fused = one launch per step (mhppo_rollout_step_fused; "
                                     "fused_kernel = its dispatch-attached kernel time), product = the "
-                                    "product's collect (one_chain loops replay a captured HIP graph)"},
+                                    "product's collect (its step loop replays a captured HIP graph)"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)

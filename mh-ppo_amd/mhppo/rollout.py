@@ -49,9 +49,10 @@ def default_parts(n_envs, valu_policy=False):
 
 def default_graph():
     """Replay the one-chain step loop from a captured HIP graph (RolloutGPU.collect) unless
-    MHPPO_ROLLOUT_GRAPH=0 (A/B)."""
+    MHPPO_ROLLOUT_GRAPH=0; =2 also captures the two-stream parts loop (measured no faster at
+    config 3: 64.5-65.2 us per step either way, profiles/r04_host/graph_parts_ab.txt)."""
     import os
-    return os.environ.get("MHPPO_ROLLOUT_GRAPH", "1") != "0"
+    return {"0": 0, "2": 2}.get(os.environ.get("MHPPO_ROLLOUT_GRAPH", "1"), 1)
 
 
 def default_fused():
@@ -113,7 +114,7 @@ class RolloutGPU:
         self._bufs = b
         # captured one-chain step loops, keyed by what their launches bake in (collect)
         self._graphs = {}
-        self.use_graph = dev.type == "cuda" and default_graph()
+        self.use_graph = default_graph() if dev.type == "cuda" else 0
         # parts > 1: part p > 0 steps on its own stream (created once), part 0 on the caller's
         self._side = [torch.cuda.Stream(device=dev) for _ in range(self.parts - 1)] if dev.type == "cuda" else []
 
@@ -193,13 +194,35 @@ class RolloutGPU:
             if step_events is not None:
                 step_events[t][1].record()
 
+    def _parts_loop(self, L, mx, mw, nparts, main):
+        """Two-stream rollout: the parts' step chains (policy -> env step -> policy ...) are
+        independent, so one part's policy MFMA work fills the CUs that another part's
+        latency-bound env step leaves idle (one wave per SIMD, the launch lasting as long as its
+        slowest wave).  Part 0 on `main`, part p > 0 on side stream p - 1, forked from and joined
+        back to `main`.  The same kernels and results as the one-chain loop."""
+        forked = torch.cuda.Event()
+        forked.record(main)
+        for side in self._side[:nparts - 1]:
+            side.wait_event(forked)
+        streams = [main.cuda_stream] + [side.cuda_stream for side in self._side[:nparts - 1]]
+        for t in range(self.T):
+            if self.P == 1:  # features straight into the step's record (include/mhppo.h)
+                self._bufs.feat_c = self.obs_c[t].data_ptr()
+            for part, sp in enumerate(streams):
+                _lib.check(L.mhppo_rollout_policy_part(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                                       ctypes.byref(self._bufs), part, sp))
+                _lib.check(L.mhppo_rollout_sample_env_part(self.venv.handle, _lib.ptr(self.eps[t]), t,
+                                                           ctypes.byref(self._bufs), part, sp))
+        for side in self._side[:nparts - 1]:
+            main.wait_stream(side)
+
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
                 eps_tape=None, step_events=None, parts=None, fused=None, graph=None):
         """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
         replay recorded draws (parity mode); otherwise Philox noise is drawn.  fused: the one-launch
         step (default: self.fused; needs self.fused_ok).  Unfused, parts: 1 forces the one-chain
         loop for this call (default: self.parts); step_events implies it.  step_events brackets
-        each step's env-step launch (the fused launch when fused).  graph: replay the one-chain loop
+        each step's env-step launch (the fused launch when fused).  graph: replay the step loop
         from a captured HIP graph (default: self.use_graph; pass False while mhppo_kernel_timing is
         on — graph nodes carry no timing events)."""
         L = _lib.lib()
@@ -222,18 +245,26 @@ class RolloutGPU:
         st = _lib.stream_ptr(device=dev)
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
-        graph = self.use_graph if graph is None else (bool(graph) and dev.type == "cuda")
-        if nparts == 1 and step_events is None and graph:
-            # The one-chain loop's 80 (fused) or 160 launches as one captured HIP graph, replayed:
-            # the same kernels and arguments (the pointers, step indices and the actors' mean / std
-            # are baked into the graph's nodes and key it), without the per-launch host work that
-            # leaves small-N steps launch-bound.
-            key = (fused, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
+        if graph is None:  # the default: the one-chain loop (and with MHPPO_ROLLOUT_GRAPH=2 the parts loop)
+            graph = bool(self.use_graph) and (nparts == 1 or fused or self.use_graph == 2)
+        graph = bool(graph) and dev.type == "cuda"
+        if step_events is None and graph:
+            # The step loop's launches (one chain: 80 fused or 160; parts: 160 per part on their
+            # streams, forked from and joined back to the capture stream) as one captured HIP
+            # graph, replayed: the same kernels and arguments (the pointers, step indices and the
+            # actors' mean / std are baked into the graph's nodes and key it), without the
+            # per-launch host work — which at small N is the step's time, and at large N keeps the
+            # host from queueing the bucketing until the rollout has nearly finished.
+            key = (fused, nparts, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._step_loop(L, mx, mw, fused, _lib.stream_ptr(device=dev), None)
+                    cap = torch.cuda.current_stream(dev)
+                    if fused or nparts == 1:
+                        self._step_loop(L, mx, mw, fused, cap.cuda_stream, None)
+                    else:
+                        self._parts_loop(L, mx, mw, nparts, cap)
                 if len(self._graphs) > 8:
                     self._graphs.clear()
                 self._graphs[key] = g
@@ -241,26 +272,7 @@ class RolloutGPU:
         elif fused or nparts == 1:
             self._step_loop(L, mx, mw, fused, st, step_events)
         else:
-            # Two-stream rollout: the parts' step chains (policy -> env step -> policy ...) are
-            # independent, so one part's policy MFMA work fills the CUs that another part's
-            # latency-bound env step leaves idle (one wave per SIMD, the launch lasting as long as
-            # its slowest wave).  The same kernels and results as the one-chain loop below.
-            main = torch.cuda.current_stream(dev)
-            forked = torch.cuda.Event()
-            forked.record(main)
-            for side in self._side[:nparts - 1]:
-                side.wait_event(forked)
-            streams = [st] + [side.cuda_stream for side in self._side[:nparts - 1]]
-            for t in range(self.T):
-                if self.P == 1:  # features straight into the step's record (include/mhppo.h)
-                    self._bufs.feat_c = self.obs_c[t].data_ptr()
-                for part, sp in enumerate(streams):
-                    _lib.check(L.mhppo_rollout_policy_part(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
-                                                           ctypes.byref(self._bufs), part, sp))
-                    _lib.check(L.mhppo_rollout_sample_env_part(self.venv.handle, _lib.ptr(self.eps[t]), t,
-                                                               ctypes.byref(self._bufs), part, sp))
-            for side in self._side[:nparts - 1]:
-                main.wait_stream(side)
+            self._parts_loop(L, mx, mw, nparts, torch.cuda.current_stream(dev))
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
         # obs_c/act/logp/rew: [N, S, T(, 13)] views of the time-major buffers (*_tm)
         return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,

@@ -222,19 +222,19 @@ def test_fused_supported_shapes():
     assert not RolloutGPU(VecCrosswalk("coop", 64, 2, 2, 2)).fused_ok
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_graph_replay_equals_eager(fused):
+@pytest.mark.parametrize("fused,parts,N", [(False, 1, 1000), (True, 1, 1000), (False, 2, 4000)])
+def test_graph_replay_equals_eager(fused, parts, N):
     """RolloutGPU.collect(graph=True): the one-chain step loop captured once as a HIP graph and
     replayed gives bit-identical records and env state to the eager launches — over two
     iterations with new noise and with the actors' weights changed in place in between (the graph
-    reads the live weights), and a new graph for other actor objects."""
+    reads the live weights); the two-stream parts loop (forked / joined inside the capture) too."""
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
     from mhppo.rollout import RolloutGPU
     outs = []
     for graph in (False, True):
-        venv = VecCrosswalk("coop", 1000, 2, 1, 2, seed_base=77)
-        ro = RolloutGPU(venv, parts=1, fused=fused)
+        venv = VecCrosswalk("coop", N, 2, 1, 2, seed_base=77)
+        ro = RolloutGPU(venv, parts=parts, fused=fused)
         torch.manual_seed(9)
         ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
         aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
