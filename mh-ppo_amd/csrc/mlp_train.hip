@@ -910,6 +910,15 @@ __device__ __forceinline__ void macc6_w(const F3 &a, const F3 &b, f32x16 &c) { X
 __device__ __forceinline__ void macc6_16_w(const F3 &a, const F3 &b, f32x4 &c) { X3_MACC6_W("v_mfma_f32_16x16x32_bf16"); }
 #undef X3_MACC6_W
 #undef X3_MACC6_BODY
+// C += A B for a B whose mid / lo parts are zero (the one-hot bias-sum columns: bf16 1.0 is exact),
+// three products, smallest first, accumulator in AGPRs.  Volatile: its A may be a fragment an
+// earlier asm block read, and it must stay behind the wait that completed it.
+__device__ __forceinline__ void macc3(const F3 &a, const u32x4 &b, f32x16 &c) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %3, %4, %0\n\tv_mfma_f32_32x32x16_bf16 %0, %2, %4, %0\n\t"
+               "v_mfma_f32_32x32x16_bf16 %0, %1, %4, %0"
+               : "+a"(c)
+               : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(b));
+}
 // before the accumulators are read: the last MFMA's result latency (>= 18 passes)
 __device__ __forceinline__ void macc_drain(f32x16 &a, f32x16 &b, f32x16 &c, f32x16 &d, f32x4 &e, f32x4 &f) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b), "+a"(c), "+a"(d), "+a"(e), "+a"(f));
@@ -989,6 +998,18 @@ __device__ __forceinline__ void put_t(float *T, const f32x16 &v, int l) {
 #pragma unroll
   for (int r = 0; r < 16; r++) b[((r & 3) + 8 * (r >> 2)) * TS] = v[r];
 }
+#ifdef MHPPO_X3_PROBE_NOSUMS
+// A/B probe only (wrong bias gradients): what the per-tile LDS row sums cost
+#define X3_ROWSUM(k, v) radd(k, (v)[0] + (v)[5])
+#else
+#define X3_ROWSUM(k, v) \
+  do {                   \
+    put_t(T, v, l);      \
+    lds_order();         \
+    radd(k, half_row_sum(T, l)); \
+    lds_order();         \
+  } while (0)
+#endif
 __device__ __forceinline__ float half_row_sum(const float *T, int l) {
   const float4 *p = reinterpret_cast<const float4 *>(T + (l & 31) * TS + 16 * (l >> 5));
   float s = 0.0f;
@@ -1112,7 +1133,11 @@ struct WaveSlot {
 // same wave, need those registers) — and then dW2 cannot carry its image reads in its MFMA gaps.
 // HB: the backward (W^T) fragments are held in registers (not with two nets in one wave).
 // G: the net's geometry (inputs, outputs); K_CHOICE: the choice actor (two outputs, softmax pair).
-template <int KIND, bool HF, bool HB, class G>
+// BS: the bias gradients dB3 / dB2 as MFMA row sums of the d3 / d2 image fragments the weight
+// gradients already read (a one-hot B column each, three products: one 16-register accumulator)
+// instead of a per-tile LDS transpose and VALU sum each (probe: -5.6 % critic / -8.4 % actor
+// tile time without those sums, profiles/r04_x3_bs/).
+template <int KIND, bool HF, bool HB, class G, bool BS = false>
 struct Pass {
   static constexpr int KS1 = G::KS1, NOUT = G::NOUT;
   static_assert(NOUT == (KIND == K_CHOICE ? 2 : 1), "outputs");
@@ -1125,6 +1150,8 @@ struct Pass {
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
   f32x16 gW2a, gW2b, gW3a, gW3b;
   f32x4 gW1t[KS1][2];
+  f32x16 gBS;    // BS: column 0 = dB3, 1 = dB2[0:32], 2 = dB2[32:64] (rows = out features)
+  u32x4 oh[3];   // BS: B fragments with bf16 1.0 in column q only
   // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4[0] gB4[0] gW4[1] gB4[1]
   float gsum[7];
   // float64 loss / advantage sums in registers (lanes kh == 0), folded once after the loop: an
@@ -1161,6 +1188,13 @@ struct Pass {
     for (int c = 0; c < KS1; c++) gW1t[c][0] = gW1t[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < 7; k++) gsum[k] = 0.f;
     dsum0 = dsum1 = dsum2 = 0.0;
+    if constexpr (BS) {
+      gBS = zero16();
+      for (int q = 0; q < 3; q++) {
+        const uint32_t v = j == q ? 0x3f803f80u : 0u;
+        oh[q] = u32x4{v, v, v, v};
+      }
+    }
   }
   __device__ __forceinline__ F3 fw2(int t, int s) const {
     if constexpr (HF) return wf2[t][s];
@@ -1327,23 +1361,14 @@ struct Pass {
       if constexpr (NOUT == 2) d3[r] = (h3[r] > 0.0f) ? fmaf(w4v1[r], dy1, w4v[r] * dy0) : 0.0f;
       else d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
     }
-    put_t(T, g, l);
-    lds_order();
-    radd(3, half_row_sum(T, l));
-    lds_order();
+    X3_ROWSUM(3, g);
     if constexpr (NOUT == 2) {
       f32x16 g1;
 #pragma unroll
       for (int r = 0; r < 16; r++) g1[r] = dy1 * h3[r];
-      put_t(T, g1, l);
-      lds_order();
-      radd(5, half_row_sum(T, l));
-      lds_order();
+      X3_ROWSUM(5, g1);
     }
-    put_t(T, d3, l);
-    lds_order();
-    radd(2, half_row_sum(T, l));
-    lds_order();
+    if constexpr (!BS) X3_ROWSUM(2, d3);
     x3_phase();
     MHPPO_MARK(5);
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
@@ -1367,6 +1392,10 @@ struct Pass {
       macc6_rd<true, 16 * IM_ROWB>(ad0, hb0, gW3b, hb1, imr);
       macc6_w(ad1, hb1, gW3b);
     }
+    if constexpr (BS) {
+      macc3(ad0, oh[0], gBS);
+      macc3(ad1, oh[0], gBS);
+    }
     lds_order();
     x3_phase();
     MHPPO_MARK(6);
@@ -1378,14 +1407,10 @@ struct Pass {
     d2b = mfma6(bw3(1, 1), d3f1, d2b);
     relu_mask(d2a, h2a);
     relu_mask(d2b, h2b);
-    put_t(T, d2a, l);
-    lds_order();
-    radd(0, half_row_sum(T, l));
-    lds_order();
-    put_t(T, d2b, l);
-    lds_order();
-    radd(1, half_row_sum(T, l));
-    lds_order();
+    if constexpr (!BS) {
+      X3_ROWSUM(0, d2a);
+      X3_ROWSUM(1, d2b);
+    }
     x3_phase();
     MHPPO_MARK(7);
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
@@ -1415,6 +1440,12 @@ struct Pass {
         macc6_rd<true, O_IM2>(da1, bh1, gW2a, db0, imr);
         macc6_rd<true, O_IM2 + 16 * IM_ROWB>(db0, bh0, gW2b, db1, imr);
         macc6_w(db1, bh1, gW2b);
+        if constexpr (BS) {  // every fragment complete: macc6_w waited for db1, the blocks before for the rest
+          macc3(da0, oh[1], gBS);
+          macc3(da1, oh[1], gBS);
+          macc3(db0, oh[2], gBS);
+          macc3(db1, oh[2], gBS);
+        }
       }
       lds_order();
     } else {  // (the forward weight fragments are held: no registers for the reads ahead)
@@ -1428,16 +1459,30 @@ struct Pass {
       lds_order();
       img_write(imw, f0, f1);
       lds_order();
-      macc6(img_read(imr, 0), bh0, gW2a);
-      macc6(img_read(imr, 1), bh1, gW2a);
+      {
+        const F3 da0 = img_read(imr, 0), da1 = img_read(imr, 1);
+        macc6(da0, bh0, gW2a);
+        macc6(da1, bh1, gW2a);
+        if constexpr (BS) {
+          macc3(da0, oh[1], gBS);
+          macc3(da1, oh[1], gBS);
+        }
+      }
       lds_order();
       const F3 f2 = split_step(d2b, 0), f3 = split_step(d2b, 1);
       d1 = mfma6(bw2(2), f2, d1);
       d1 = mfma6(bw2(3), f3, d1);
       img_write(imw, f2, f3);
       lds_order();
-      macc6(img_read(imr, 0), bh0, gW2b);
-      macc6(img_read(imr, 1), bh1, gW2b);
+      {
+        const F3 db0 = img_read(imr, 0), db1 = img_read(imr, 1);
+        macc6(db0, bh0, gW2b);
+        macc6(db1, bh1, gW2b);
+        if constexpr (BS) {
+          macc3(db0, oh[2], gBS);
+          macc3(db1, oh[2], gBS);
+        }
+      }
       lds_order();
     }
     relu_mask(d1, h1);
@@ -1485,6 +1530,7 @@ struct Pass {
     const int l = ws.l, j = ws.j, kh = ws.kh, G_ = ws.G;
     if constexpr (KS1 == 1) macc_drain(gW2a, gW2b, gW3a, gW3b, gW1t[0][0], gW1t[0][1]);
     else macc_drain2(gW2a, gW2b, gW3a, gW3b, gW1t[0][0], gW1t[0][1], gW1t[KS1 - 1][0], gW1t[KS1 - 1][1]);
+    if constexpr (BS) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(gBS));
     float gB2a = gsum[0], gB2b = gsum[1], gB3 = gsum[2], gW4 = gsum[3], gB4 = gsum[4];
     float gW41 = gsum[5], gB41 = gsum[6];
 #pragma unroll
@@ -1514,11 +1560,20 @@ struct Pass {
     gW4 += __shfl_xor(gW4, 32);
     if (NOUT == 2) gW41 += __shfl_xor(gW41, 32);
     if (kh == 0) {
-      gp[P.B2 + j] = gB2a;
-      gp[P.B2 + 32 + j] = gB2b;
-      gp[P.B3 + j] = gB3;
+      if constexpr (!BS) {
+        gp[P.B2 + j] = gB2a;
+        gp[P.B2 + 32 + j] = gB2b;
+        gp[P.B3 + j] = gB3;
+      }
       gp[P.W4 + j] = gW4;
       if (NOUT == 2) gp[P.W4 + 32 + j] = gW41;
+    }
+    if constexpr (BS) {  // column q of the row-sum accumulator: lanes q, q + 32 (rows: feat(r, l))
+      if (j < 3) {
+        const int base = j == 0 ? P.B3 : (j == 1 ? P.B2 : P.B2 + 32);
+#pragma unroll
+        for (int r = 0; r < 16; r++) gp[base + feat(r, l)] = gBS[r];
+      }
     }
     float b4s0 = gB4, b4s1 = gB41;
 #pragma unroll
@@ -1665,6 +1720,14 @@ __device__ __forceinline__ void fold_partials(PassT &p, const WaveSlot<G> &ws, c
 }
 }  // namespace x3
 
+#ifndef MHPPO_X3_BS
+#define MHPPO_X3_BS 7  // bits: 1 critic passes, 2 actor passes, 4 the fused pair (A/B builds override)
+#endif
+constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3_BS_PAIR = MHPPO_X3_BS & 4;
+#ifndef MHPPO_X3_CRITIC_HF
+#define MHPPO_X3_CRITIC_HF 1  // the 13-input critic holds its forward fragments (A/B builds override)
+#endif
+constexpr bool X3_CRITIC_HF = MHPPO_X3_CRITIC_HF;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
@@ -1684,7 +1747,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   __syncthreads();
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
-  Pass<KIND, KIND == K_CRITIC && G::NIC == NIN_CONT, true, G> p;
+  Pass<KIND, X3_CRITIC_HF && KIND == K_CRITIC && G::NIC == NIN_CONT, true, G,
+       (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR)>
+      p;
   p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
   if (KIND != K_CRITIC) adv_norm(stats, m_global, meanf, stdf);
@@ -1728,8 +1793,8 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   stage_net<G>(Wa, L8, tid, NIN_CONT);
   stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
-  Pass<K_CONT, false, PAIR_HB, G> pa;
-  Pass<K_CRITIC, false, PAIR_HB, G> pc;
+  Pass<K_CONT, false, PAIR_HB, G, X3_BS_PAIR> pa;
+  Pass<K_CRITIC, false, PAIR_HB, G, X3_BS_PAIR> pc;
   pa.init(L8, ws);
   pc.init(L8 + G::NET_B, ws);
   float meanf, stdf;

@@ -6,7 +6,7 @@ set -o pipefail
 for v in "$@"; do
   if [ "$v" = base ]; then lib=""; else lib="build_ab/$v/libmhppo.so"; fi
   echo "== $v split"
-  MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 || exit 1
+  MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 $AB_ARGS || exit 1
   if [ -n "$AB_EXACT" ]; then
     echo "== $v exact f32"
     MHPPO_LIB=$lib timeout -k 10 120 python tools/bench_mlp_train.py --reps 10 --exact || exit 1
