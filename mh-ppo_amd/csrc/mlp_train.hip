@@ -1133,6 +1133,10 @@ struct WaveSlot {
 // same wave, need those registers) — and then dW2 cannot carry its image reads in its MFMA gaps.
 // HB: the backward (W^T) fragments are held in registers (not with two nets in one wave).
 // G: the net's geometry (inputs, outputs); K_CHOICE: the choice actor (two outputs, softmax pair).
+#ifndef MHPPO_X3_W4R
+#define MHPPO_X3_W4R 1  // A/B builds override
+#endif
+constexpr bool X3_W4R = MHPPO_X3_W4R;
 // BS: the bias gradients dB3 / dB2 as MFMA row sums of the d3 / d2 image fragments the weight
 // gradients already read (a one-hot B column each, three products: one 16-register accumulator)
 // instead of a per-tile LDS transpose and VALU sum each (probe: -5.6 % critic / -8.4 % actor
@@ -1152,6 +1156,12 @@ struct Pass {
   f32x4 gW1t[KS1][2];
   f32x16 gBS;    // BS: column 0 = dB3, 1 = dB2[0:32], 2 = dB2[32:64] (rows = out features)
   u32x4 oh[3];   // BS: B fragments with bf16 1.0 in column q only
+  // W4R (the actor passes: registers to spare): dW4 = sum over rows of dy h3 accumulated per lane
+  // and register across the wave's tiles (one FMA per element) and summed over the lanes once, in
+  // finish, instead of a per-tile LDS transpose (probe: -2.7 % actor tile time without that sum)
+  // (the continuous actor: the choice actor's second output would spill the K = 32 geometry)
+  static constexpr bool W4R = KIND == K_CONT && X3_W4R;
+  f32x16 gW4r, gW4r1;
   // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4[0] gB4[0] gW4[1] gB4[1]
   float gsum[7];
   // float64 loss / advantage sums in registers (lanes kh == 0), folded once after the loop: an
@@ -1188,6 +1198,10 @@ struct Pass {
     for (int c = 0; c < KS1; c++) gW1t[c][0] = gW1t[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < 7; k++) gsum[k] = 0.f;
     dsum0 = dsum1 = dsum2 = 0.0;
+    if constexpr (W4R) {
+      gW4r = zero16();
+      if constexpr (NOUT == 2) gW4r1 = zero16();
+    }
     if constexpr (BS) {
       gBS = zero16();
       for (int q = 0; q < 3; q++) {
@@ -1294,12 +1308,17 @@ struct Pass {
         if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 128), 4 * j, 0, 0);
         const float a = rt - v;
         const float d = v - rt;
+#ifdef MHPPO_X3_PROBE_NOLOSS
+        dy0 = d * (float)inv_m;  // A/B probe only: no float64 loss / advantage sums
+        dsum0 += a;
+#else
         if (kh == 0) {
           dsum0 += (double)d * (double)d;
           dsum1 += (double)a;
           dsum2 += (double)a * (double)a;
         }
         dy0 = (float)(2.0 * inv_m * (double)d);
+#endif
       } else if constexpr (KIND == K_CONT) {
         const float t = tanhf(y0);
         const float mu = t * out_std + out_mean;
@@ -1308,11 +1327,17 @@ struct Pass {
         const float diff = (float)((double)slot[G::IN_S1 + j] - (double)mu);
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
+#ifdef MHPPO_X3_PROBE_NOLOSS
+        const float rf = __expf(lp - slot[G::IN_S1 + 32 + j]);  // A/B probe only: float ratio
+        dsum0 += rf * A;
+        const float dmu = (float)inv_m * rf * A * x * MVN_INV_L;
+#else
         const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
         double dfdr;
         const double f = surr_and_grad(r, (double)A, dfdr);
         if (kh == 0) dsum0 += f;
         const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+#endif
         dy0 = (dmu * out_std) * (1.0f - t * t);
       } else {
         // choice actor (train_model_d :818-851): softmax over the pair (as torch: shift by the
@@ -1361,12 +1386,25 @@ struct Pass {
       if constexpr (NOUT == 2) d3[r] = (h3[r] > 0.0f) ? fmaf(w4v1[r], dy1, w4v[r] * dy0) : 0.0f;
       else d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
     }
-    X3_ROWSUM(3, g);
-    if constexpr (NOUT == 2) {
-      f32x16 g1;
+    if constexpr (W4R) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) g1[r] = dy1 * h3[r];
-      X3_ROWSUM(5, g1);
+      for (int r = 0; r < 16; r++) gW4r[r] += g[r];
+      if constexpr (NOUT == 2) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) gW4r1[r] += dy1 * h3[r];
+      }
+    } else {
+#ifdef MHPPO_X3_PROBE_NOW4
+      radd(3, g[0]);  // A/B probe only: the dW4 row sum removed (wrong dW4)
+#else
+      X3_ROWSUM(3, g);
+#endif
+      if constexpr (NOUT == 2) {
+        f32x16 g1;
+#pragma unroll
+        for (int r = 0; r < 16; r++) g1[r] = dy1 * h3[r];
+        X3_ROWSUM(5, g1);
+      }
     }
     if constexpr (!BS) X3_ROWSUM(2, d3);
     x3_phase();
@@ -1565,8 +1603,25 @@ struct Pass {
         gp[P.B2 + 32 + j] = gB2b;
         gp[P.B3 + j] = gB3;
       }
-      gp[P.W4 + j] = gW4;
-      if (NOUT == 2) gp[P.W4 + 32 + j] = gW41;
+      if constexpr (!W4R) {
+        gp[P.W4 + j] = gW4;
+        if (NOUT == 2) gp[P.W4 + 32 + j] = gW41;
+      }
+    }
+    if constexpr (W4R) {  // register r of lane (row j, half kh) holds feature feat(r, l): sum over j
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        float v = gW4r[r], v1 = NOUT == 2 ? gW4r1[r] : 0.0f;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          v += __shfl_xor(v, o);
+          if constexpr (NOUT == 2) v1 += __shfl_xor(v1, o);
+        }
+        if (j == 0) {
+          gp[P.W4 + feat(r, l)] = v;
+          if constexpr (NOUT == 2) gp[P.W4 + 32 + feat(r, l)] = v1;
+        }
+      }
     }
     if constexpr (BS) {  // column q of the row-sum accumulator: lanes q, q + 32 (rows: feat(r, l))
       if (j < 3) {
@@ -1684,7 +1739,12 @@ __device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int
     const int nrows = (int)min((int64_t)32, M - row0);
     float *slot = ws.inb + cb * G::IN_SZ;
     const int64_t nxt = tile + nw;
+#ifdef MHPPO_X3_PROBE_NODMA
+    cb = 0;  // A/B probe only: every tile reuses the first tile's inputs (no DMA after it)
+    if (false) {
+#else
     if (nxt < nfull) {
+#endif
       prefetch(ws.inb + (cb ^ 1) * G::IN_SZ, nxt * 32);
       if constexpr (FIXED) wait_vmcnt<prefetch_ops<KIND>()>();
       else wait_vmcnt<prefetch_g_ops<KIND, G>()>();
