@@ -1141,7 +1141,12 @@ constexpr bool X3_W4R = MHPPO_X3_W4R;
 // gradients already read (a one-hot B column each, three products: one 16-register accumulator)
 // instead of a per-tile LDS transpose and VALU sum each (probe: -5.6 % critic / -8.4 % actor
 // tile time without those sums, profiles/r04_x3_bs/).
-template <int KIND, bool HF, bool HB, class G, bool BS = false>
+// DH2F: the on-chain dH2 MFMAs issued before the off-chain dW3 block (the h2 image splits in their
+// shadow); XCE: dW1's first input-column split issued before the dH1 MFMAs.  Measured per kernel
+// (profiles/r04_x3_bs/ab_order.txt): continuous actor both (-1.9 %), fused pair DH2F (-1.6 %), the
+// critic neither (its 512 registers: +3 % with either).
+template <int KIND, int HF, bool HB, class G, bool BS = false, bool DH2F = false, bool XCE = false,
+          bool W4R_ = KIND == K_CONT>
 struct Pass {
   static constexpr int KS1 = G::KS1, NOUT = G::NOUT;
   static_assert(NOUT == (KIND == K_CHOICE ? 2 : 1), "outputs");
@@ -1160,7 +1165,7 @@ struct Pass {
   // and register across the wave's tiles (one FMA per element) and summed over the lanes once, in
   // finish, instead of a per-tile LDS transpose (probe: -2.7 % actor tile time without that sum)
   // (the continuous actor: the choice actor's second output would spill the K = 32 geometry)
-  static constexpr bool W4R = KIND == K_CONT && X3_W4R;
+  static constexpr bool W4R = W4R_ && X3_W4R;
   f32x16 gW4r, gW4r1;
   // bias-gradient half-row sums (lane j, half kh): gB2a gB2b gB3 gW4[0] gB4[0] gW4[1] gB4[1]
   float gsum[7];
@@ -1184,9 +1189,11 @@ struct Pass {
     b40 = uniform_f(F[G::F_B4]);
     b41 = NOUT == 2 ? uniform_f(F[G::F_B4 + 1]) : 0.0f;
     // loop-invariant weight fragments read from LDS once
-    if constexpr (HF) {
+    if constexpr (HF & 1) {
       for (int t = 0; t < 2; t++)
         for (int s = 0; s < 2; s++) wf2[t][s] = w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
+    }
+    if constexpr (HF & 2) {
       for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
     }
     if constexpr (HB) {
@@ -1211,11 +1218,11 @@ struct Pass {
     }
   }
   __device__ __forceinline__ F3 fw2(int t, int s) const {
-    if constexpr (HF) return wf2[t][s];
+    if constexpr (HF & 1) return wf2[t][s];
     else return w_fwd<W2_ROWB, W2_PART>(w2row, t, s);
   }
   __device__ __forceinline__ F3 fw3(int s) const {
-    if constexpr (HF) return wf3[s];
+    if constexpr (HF & 2) return wf3[s];
     else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   }
   __device__ __forceinline__ F3 bw3(int t, int s) const {
@@ -1411,6 +1418,15 @@ struct Pass {
     MHPPO_MARK(5);
     // ---- dW3 = sum over rows of d3 (x) h2: A = d3 image, B = h2a / h2b images
     const F3 d3f0 = split_step(d3, 0), d3f1 = split_step(d3, 1);
+    // dH2^T = W3^T . dH3^T (below, or here with DH2F: issued before the dW3 block)
+    f32x16 d2a = zero16(), d2b = zero16();
+    auto dh2 = [&]() {
+      d2a = mfma6(bw3(0, 0), d3f0, d2a);
+      d2a = mfma6(bw3(0, 1), d3f1, d2a);
+      d2b = mfma6(bw3(1, 0), d3f0, d2b);
+      d2b = mfma6(bw3(1, 1), d3f1, d2b);
+    };
+    if constexpr (DH2F) dh2();
     img_write(imw, d3f0, d3f1);
     lds_order();
     const F3 ad0 = img_read(imr, 0), ad1 = img_read(imr, 1);
@@ -1438,11 +1454,7 @@ struct Pass {
     x3_phase();
     MHPPO_MARK(6);
     // ---- dH2^T = W3^T . dH3^T, masked by h2 > 0; dB2 = row sums
-    f32x16 d2a = zero16(), d2b = zero16();
-    d2a = mfma6(bw3(0, 0), d3f0, d2a);
-    d2a = mfma6(bw3(0, 1), d3f1, d2a);
-    d2b = mfma6(bw3(1, 0), d3f0, d2b);
-    d2b = mfma6(bw3(1, 1), d3f1, d2b);
+    if constexpr (!DH2F) dh2();
     relu_mask(d2a, h2a);
     relu_mask(d2b, h2b);
     if constexpr (!BS) {
@@ -1451,9 +1463,22 @@ struct Pass {
     }
     x3_phase();
     MHPPO_MARK(7);
+    // the B operand of dW1's input columns 16c .. 16c + 15: rows 8G .. 8G + 7 of column 16c + n
+    auto xcols = [&](int c) {
+      float xv[8];
+      const int n = 16 * c + (l & 15);
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const float v = Xs[(8 * G_ + q) * nin + (n < nin ? n : 0)];
+        xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
+      }
+      return split8(xv);
+    };
+    F3 xb0;  // XCE: dW1's first input-column split, issued ahead of the dH1 MFMAs (into their shadow)
+    if constexpr (XCE) xb0 = xcols(0);
     // ---- dH1^T = W2^T . dH2^T, masked by h1 > 0; dW2 = sum over rows of d2 (x) h1
     f32x16 d1 = zero16();
-    if constexpr (!HF) {
+    if constexpr (HF != 3) {
       const F3 f0 = split_step(d2a, 0), f1 = split_step(d2a, 1);
       d1 = mfma6(bw2(0), f0, d1);
       d1 = mfma6(bw2(1), f1, d1);
@@ -1533,18 +1558,9 @@ struct Pass {
     img_write(imw, split_step(d1, 0), split_step(d1, 1));
     lds_order();
     {
-      // the B operand of input columns 16c .. 16c + 15: rows 8G .. 8G + 7 of column 16c + n
-      auto xcols = [&](int c) {
-        float xv[8];
-        const int n = 16 * c + (l & 15);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const float v = Xs[(8 * G_ + q) * nin + (n < nin ? n : 0)];
-          xv[q] = n < nin ? v : (n == nin ? 1.0f : 0.0f);
-        }
-        return split8(xv);
-      };
-      const F3 b = xcols(0);
+      F3 b;
+      if constexpr (XCE) b = xb0;
+      else b = xcols(0);
       const F3 a0 = tr_pair<IM_PART>(imr16, 4 * IM_ROWB);
       F3 a1;
       macc6_16_rd<false, 32>(a0, b, gW1t[0][0], a1, imr16);
@@ -1784,10 +1800,13 @@ __device__ __forceinline__ void fold_partials(PassT &p, const WaveSlot<G> &ws, c
 #define MHPPO_X3_BS 7  // bits: 1 critic passes, 2 actor passes, 4 the fused pair (A/B builds override)
 #endif
 constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3_BS_PAIR = MHPPO_X3_BS & 4;
-#ifndef MHPPO_X3_CRITIC_HF
-#define MHPPO_X3_CRITIC_HF 1  // the 13-input critic holds its forward fragments (A/B builds override)
+#ifndef MHPPO_X3_CRIT
+// the 13-input critic pass: bits 0-1 = forward fragments held in registers (1 W2, 2 W3), bit 2 =
+// dW4 in registers, bit 3 = DH2F + XCE ordering (A/B builds override)
+#define MHPPO_X3_CRIT 13  // W2's forward fragments held, dW4 in registers, DH2F + XCE (ab_crit.txt)
 #endif
-constexpr bool X3_CRITIC_HF = MHPPO_X3_CRITIC_HF;
+constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
+constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
@@ -1807,8 +1826,10 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   __syncthreads();
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
-  Pass<KIND, X3_CRITIC_HF && KIND == K_CRITIC && G::NIC == NIN_CONT, true, G,
-       (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR)>
+  constexpr bool C13 = KIND == K_CRITIC && G::NIC == NIN_CONT;  // the 13-input critic
+  Pass<KIND, C13 ? X3_CRIT_HF : 0, true, G, (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR),
+       KIND == K_CONT || (C13 && X3_CRIT_ORD), KIND == K_CONT || (C13 && X3_CRIT_ORD),
+       KIND == K_CONT || (C13 && X3_CRIT_W4R)>
       p;
   p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
@@ -1853,8 +1874,8 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   stage_net<G>(Wa, L8, tid, NIN_CONT);
   stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
-  Pass<K_CONT, false, PAIR_HB, G, X3_BS_PAIR> pa;
-  Pass<K_CRITIC, false, PAIR_HB, G, X3_BS_PAIR> pc;
+  Pass<K_CONT, false, PAIR_HB, G, X3_BS_PAIR, true> pa;
+  Pass<K_CRITIC, false, PAIR_HB, G, X3_BS_PAIR, true> pc;
   pa.init(L8, ws);
   pc.init(L8 + G::NET_B, ws);
   float meanf, stdf;
