@@ -1145,7 +1145,7 @@ constexpr bool X3_W4R = MHPPO_X3_W4R;
 // shadow); XCE: dW1's first input-column split issued before the dH1 MFMAs.  Measured per kernel
 // (profiles/r04_x3_bs/ab_order.txt): continuous actor both (-1.9 %), fused pair DH2F (-1.6 %), the
 // critic neither (its 512 registers: +3 % with either).
-template <int KIND, int HF, bool HB, class G, bool BS = false, bool DH2F = false, bool XCE = false,
+template <int KIND, int HF, int HB, class G, bool BS = false, bool DH2F = false, bool XCE = false,
           bool W4R_ = KIND == K_CONT>
 struct Pass {
   static constexpr int KS1 = G::KS1, NOUT = G::NOUT;
@@ -1196,9 +1196,11 @@ struct Pass {
     if constexpr (HF & 2) {
       for (int s = 0; s < 4; s++) wf3[s] = w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
     }
-    if constexpr (HB) {
+    if constexpr (HB & 1) {
       for (int t = 0; t < 2; t++)
         for (int s = 0; s < 2; s++) wb3[t][s] = w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
+    }
+    if constexpr (HB & 2) {
       for (int s = 0; s < 4; s++) wb2[s] = w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
     }
     gW2a = zero16(), gW2b = zero16(), gW3a = zero16(), gW3b = zero16();
@@ -1226,11 +1228,11 @@ struct Pass {
     else return w_fwd<W3_ROWB, W3_PART>(w3row, 0, s);
   }
   __device__ __forceinline__ F3 bw3(int t, int s) const {
-    if constexpr (HB) return wb3[t][s];
+    if constexpr (HB & 1) return wb3[t][s];
     else return w_bwd<W3_ROWB, W3_PART>(w3tr, t, s);
   }
   __device__ __forceinline__ F3 bw2(int s) const {
-    if constexpr (HB) return wb2[s];
+    if constexpr (HB & 2) return wb2[s];
     else return w_bwd<W2_ROWB, W2_PART>(w2tr, 0, s);
   }
 
@@ -1807,6 +1809,13 @@ constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3
 #endif
 constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
 constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
+#ifndef MHPPO_X3_ACT
+// the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
+// fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE (A/B overrides)
+#define MHPPO_X3_ACT 62  // W3's forward fragments held too (ab_act.txt: W2's -2.8 %, ab_act2.txt: W3's -1 % more)
+#endif
+constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
+constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
@@ -1827,9 +1836,10 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
   constexpr bool C13 = KIND == K_CRITIC && G::NIC == NIN_CONT;  // the 13-input critic
-  Pass<KIND, C13 ? X3_CRIT_HF : 0, true, G, (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR),
-       KIND == K_CONT || (C13 && X3_CRIT_ORD), KIND == K_CONT || (C13 && X3_CRIT_ORD),
-       KIND == K_CONT || (C13 && X3_CRIT_W4R)>
+  constexpr bool A13 = KIND == K_CONT;
+  Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : 0), A13 ? X3_ACT_HB : 3, G,
+       (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR), (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD),
+       (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD), (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R)>
       p;
   p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
@@ -1853,9 +1863,9 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
 // rows of V with V_{e+1} (each tile belongs to one wave; its inputs land one tile ahead).
 // Partials: actor at gpart[gw], critic at gpart[nw + gw] (and dpart likewise).
 #ifndef MHPPO_PAIR_HB
-#define MHPPO_PAIR_HB false
+#define MHPPO_PAIR_HB 0
 #endif
-constexpr bool PAIR_HB = MHPPO_PAIR_HB;
+constexpr int PAIR_HB = MHPPO_PAIR_HB;
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3_pair(const float *__restrict__ Wa, const float *__restrict__ Wc, const float *__restrict__ X,
                         int64_t M, const float *__restrict__ ret, float *__restrict__ V,
