@@ -1816,6 +1816,14 @@ constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 #endif
 constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
 constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
+#ifndef MHPPO_X3_CC
+#define MHPPO_X3_CC 0  // the choice critic (runtime input count), bits as MHPPO_X3_CRIT (A/B overrides)
+#endif
+#ifndef MHPPO_X3_CA
+#define MHPPO_X3_CA 0  // the choice actor: bits 0-1 forward fragments held, bit 3 DH2F + XCE
+#endif
+constexpr int X3_CC_HF = MHPPO_X3_CC & 3, X3_CA_HF = MHPPO_X3_CA & 3;
+constexpr bool X3_CC_W4R = MHPPO_X3_CC & 4, X3_CC_ORD = MHPPO_X3_CC & 8, X3_CA_ORD = MHPPO_X3_CA & 8;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3(const float *__restrict__ W, const float *__restrict__ X, int nin, int64_t M,
@@ -1837,9 +1845,11 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   // runtime input count the choice critic has no registers for them: 23-38 spills)
   constexpr bool C13 = KIND == K_CRITIC && G::NIC == NIN_CONT;  // the 13-input critic
   constexpr bool A13 = KIND == K_CONT;
-  Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : 0), A13 ? X3_ACT_HB : 3, G,
-       (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR), (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD),
-       (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD), (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R)>
+  constexpr bool CC = KIND == K_CRITIC && !C13, CA = KIND == K_CHOICE;  // the choice head's nets
+  constexpr bool ORD = (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD) || (CC && X3_CC_ORD) || (CA && X3_CA_ORD);
+  Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : (CC ? X3_CC_HF : X3_CA_HF)), A13 ? X3_ACT_HB : 3, G,
+       (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR), ORD, ORD,
+       (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R) || (CC && X3_CC_W4R)>
       p;
   p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
