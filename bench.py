@@ -4,8 +4,10 @@
 One bench "step" = one full PPO iteration on this rank's shard: one call of the product's
 Algo_PPO.train(1) (Coop-MH-PPO-scalable.py:854-917), reward-curve file writing off:
     rollout.reset() -> reset N envs + 80 rollout steps (choice head at t=0; per step:
-    policy kernel + fused sample/env-step kernel) -> returns scan -> bucketing ->
-    10 joint epochs of the three heads (cross, wait, choice) -> immediate rewards, the
+    policy kernel + fused sample/env-step kernel, two env halves on two streams; at small N
+    one chain replayed from a HIP graph) -> returns scan -> bucketing -> 10 joint epochs of
+    the three heads (cross, wait, choice; the heads' passes alternate over two streams) ->
+    immediate rewards, the
     reward-sum all-reduce and its host read (the reward curves) -> rollout.reset().
 Default workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
     Env_hybrid_multi_coop_4cars, 4 AVs (+4 IDM followers), 1 pedestrian, 2 lanes,
@@ -22,8 +24,9 @@ process touches the GPU, and relays rank 0's JSON line; under an external launch
 Extra JSON fields:
   roofline     — the dominant kernel, the fused continuous-head train kernel (k_mlp_train,
                  ~85 % of GPU time): algorithmic FLOPs per row x rows /
-                 launch duration, from HIP events on its stream inside the timed region,
-                 summed over all launches.  The kernel runs the bf16x3 split path
+                 launch duration, from HIP events on its stream around each launch of one
+                 extra training iteration run right after the timed region with the passes on
+                 one stream (concurrent launches on two streams would blur the events).  The kernel runs the bf16x3 split path
                  (six bf16 MFMAs per f32 product, f32-level accuracy), so its
                  ceiling is the bf16 dense MFMA peak / 6 = 419.4 TFLOP/s of f32-equivalent
                  work; the fraction of the f32-MFMA peak (157.3) is reported beside it.
@@ -204,9 +207,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ppo.TRAIN_EVENTS = []
-    # the env-step launches carry HIP events attached to their dispatch packets
-    # (hipExtLaunchKernelGGL): the kernel's own execution time, as rocprofv3 reports it
     t0 = time.perf_counter()
     for k in range(a.steps):
         iteration()
@@ -220,11 +220,19 @@ def main():
     dt = float(t.item())
     ms = dt / a.steps * 1e3
     value = world * N * T / (dt / a.steps)
-    # After the timed region (same process, same workload): (1) the env-step kernel over all N envs
+    # After the timed region (same process, same workload): (0) one more training iteration with the
+    # train passes on ONE stream and torch events around each launch -> roofline (the product runs
+    # the heads' passes on two streams, where one launch's events would span the other's kernel);
+    # (1) the env-step kernel over all N envs
     # with HIP events attached to its 80 launches' dispatch packets (hipExtLaunchKernelGGL: the
     # kernel's own execution, as rocprofv3 reports it) -> roofline_env; (2) the rollout's wall time
     # per step (policy + env step) with the one-chain loop and with the product's two-stream parts
     # (RolloutGPU.parts), from torch events around whole collects.
+    streams_product = ppo.TRAIN_STREAMS
+    ppo.TRAIN_STREAMS, ppo.TRAIN_EVENTS = 1, []
+    iteration()
+    torch.cuda.synchronize()
+    ppo.TRAIN_STREAMS = streams_product
     gpu = algo.rollout.gpu
     env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
     step_us, fused_kern_us = {}, None
@@ -291,7 +299,9 @@ def main():
                      "traffic": traffic, "traffic_unit": "B/launch",
                      "flops_per_row": ppo.FLOPS_PER_ROW_CONT, "rows_per_launch": tr_rows / max(len(tr), 1),
                      "launches": len(tr), "passes": sum(2 if k == 3 else 1 for k, _, _, _, _ in tr),
-                     "launch_ms": tr_ms / max(len(tr), 1)},
+                     "launch_ms": tr_ms / max(len(tr), 1),
+                     "measured_on": "one extra training iteration after the timed region, its passes on one "
+                                    f"stream (the product: heads on {streams_product} streams)"},
         "roofline_env": {"bound": "hbm", "kernel": "k_sample_env (fused select/MVN/env.step)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_env, "traffic_unit": "B/launch",

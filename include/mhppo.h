@@ -322,7 +322,8 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
  * bf16 parts (products to f32 accuracy; X must then be 16-byte aligned); kind |
  * MHPPO_TRAIN_EXACT_F32 selects the f32-MFMA kernel, whose sums are k-ordered fmaf chains
  * (wider heads always run on it).
- * Per-device workspace: calls on one device must be ordered on one stream. */
+ * Per-device, per-stream workspace (up to 4 streams per device): calls on one stream are ordered by
+ * it, calls on different streams may run concurrently (MHPPO_EINVAL for a fifth stream). */
 #define MHPPO_TRAIN_EXACT_F32 0x100
 int mhppo_mlp_train(int kind, int n_in, const float *packed, const float *X, int64_t M, const float *ret,
                     float *value, const float *act, const float *logp_old, const double *stats,

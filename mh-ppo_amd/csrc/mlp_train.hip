@@ -2007,7 +2007,12 @@ struct Work {  // per-device partial buffers (calls on one device must share one
   int nw = 0;
   int cus = 0;
 };
-Work g_work[mhppo::MAX_DEVICES];
+// per device and stream (up to WORK_STREAMS streams per device may run train passes concurrently:
+// each stream's passes reduce through their own partial buffers)
+constexpr int WORK_STREAMS = 4;
+Work g_work[mhppo::MAX_DEVICES][WORK_STREAMS];
+hipStream_t g_work_stream[mhppo::MAX_DEVICES][WORK_STREAMS];
+int g_work_used[mhppo::MAX_DEVICES] = {0};
 // partial buffers for `slots` waves' partials (a fused pair launch uses two slots per wave)
 bool ensure_work(Work &wk, int slots) {
   if (wk.nw >= slots) return true;
@@ -2023,14 +2028,21 @@ bool ensure_work(Work &wk, int slots) {
   wk.nw = slots;
   return true;
 }
-Work &device_work(int dev) {
-  Work &wk = g_work[dev];
+Work *device_work(int dev, hipStream_t s) {
+  int k = 0;
+  while (k < g_work_used[dev] && g_work_stream[dev][k] != s) k++;
+  if (k == g_work_used[dev]) {
+    if (k == WORK_STREAMS) return nullptr;
+    g_work_stream[dev][k] = s;
+    g_work_used[dev] = k + 1;
+  }
+  Work &wk = g_work[dev][k];
   if (wk.cus == 0) {
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     wk.cus = cus;
   }
-  return wk;
+  return &wk;
 }
 
 template <int KIND, int KS, bool PF>
@@ -2078,7 +2090,9 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   int dev = 0;
   CHECK_HIP(hipGetDevice(&dev));
   if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
-  Work &wk = device_work(dev);
+  Work *wkp = device_work(dev, s);
+  if (!wkp) return set_error(MHPPO_EINVAL, "train passes on more than %d streams of one device", WORK_STREAMS);
+  Work &wk = *wkp;
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
   // the choice heads' nets (up to 31 inputs) on the split-precision kernel too (wider: f32 MFMA)
   const bool split_c = !pf && !exact && n_in <= 31;
@@ -2166,7 +2180,9 @@ extern "C" int mhppo_mlp_train_pair(const float *packed_actor, const float *pack
   int dev = 0;
   CHECK_HIP(hipGetDevice(&dev));
   if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
-  Work &wk = device_work(dev);
+  Work *wkp = device_work(dev, s);
+  if (!wkp) return set_error(MHPPO_EINVAL, "train passes on more than %d streams of one device", WORK_STREAMS);
+  Work &wk = *wkp;
   const int64_t tiles = (M + 31) / 32;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(wk.cus, (tiles + x3::WAVES - 1) / x3::WAVES));
   const int nw = (int)blocks * x3::WAVES;

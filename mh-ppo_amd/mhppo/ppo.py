@@ -26,6 +26,7 @@ gradient is that of (global-mean loss restricted to its rows), so the reduced
 gradient is the full-batch gradient; Adam then runs replicated.  A rank whose shard
 of a head is empty still joins both collectives (the kernel writes a zero gradient).
 """
+import contextlib
 import os
 
 import torch
@@ -423,6 +424,24 @@ def _pair_pass(p, h, stats, sums_a, sums_c, st):
     _ev_end(ev, 3, 13, p.M)  # kind 3: a fused pair launch (two passes)
 
 
+# Heads' passes on alternating streams within an epoch step (train_epochs): head i's passes on
+# stream i % TRAIN_STREAMS (a head's actor and critic passes stay in order on one stream: the critic
+# pass e + 1 overwrites the V_e the actor pass e reads).  The heads are independent within a step, so
+# one head's launch and weight staging overlap the other's tail, partial fold and reduction
+# (mhppo_mlp_train keeps a workspace per stream).  MHPPO_TRAIN_STREAMS=1: one stream (A/B).
+TRAIN_STREAMS = max(1, int(os.environ.get("MHPPO_TRAIN_STREAMS", "2")))
+_SIDE_STREAMS = {}
+
+
+def _side_streams(dev, n):
+    if dev.type != "cuda" or n <= 0:
+        return []
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), n)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    return _SIDE_STREAMS[key]
+
+
 def train_epochs(heads, n_epochs, bucket=None):
     """n_epochs full-batch epochs of every head, run as a pipeline of n_epochs + 1 steps: step k
     runs the actor passes of epoch k - 1 and the critic passes of epoch k (a continuous head on the
@@ -438,43 +457,56 @@ def train_epochs(heads, n_epochs, bucket=None):
     dev = heads[0].obs.device
     paired = [_use_pair(h) for h in heads]
     plans = [_HeadPlan(h) if h.obs.shape[0] > 0 else None for h in heads]
-    st = _lib.stream_ptr().value if dev.type == "cuda" else None
+    main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    side = _side_streams(dev, min(TRAIN_STREAMS, H) - 1)
+    streams = [main] + side
     stats = None        # all-reduced advantage sums of the previous step's critic passes [2H]
     out = [[None, None] for _ in range(H)]
     for k in range(n_epochs + 1):
         sums = torch.zeros(2 * H, 3, dtype=torch.float64, device=dev)  # critic rows, actor rows
         crit = k < n_epochs
         trained = []
+        if side:  # the side streams start after this step's inputs (Adam, sums, stats) on main
+            fork = torch.cuda.Event()
+            fork.record(main)
+            for sd in side:
+                sd.wait_event(fork)
         for i, h in enumerate(heads):
             p = plans[i]
             sc, sa = sums[i], sums[H + i]
-            stp = stats[2 * i:2 * i + 2] if k > 0 else None
-            if p is None:  # an empty shard: zero gradients, sums unchanged (k_mlp_train's M == 0 path)
-                if k > 0:
-                    cont = h.kind == "c"
-                    k_mlp_train(KIND_CONT if cont else KIND_CHOICE, h.actor, h.obs, h.ret, h.obs.new_empty(0),
-                                h.act if (cont or h.per_row) else None, h.logp, stp,
-                                None if (cont or h.per_row) else h.counts, m_global=h.m, sums=sa, exact=h.exact)
+            sti = streams[i % len(streams)]
+            ctx = torch.cuda.stream(sti) if sti is not None else contextlib.nullcontext()
+            st = sti.cuda_stream if sti is not None else None
+            with ctx:
+                stp = stats[2 * i:2 * i + 2] if k > 0 else None
+                if p is None:  # an empty shard: zero gradients, sums unchanged (k_mlp_train's M == 0 path)
+                    if k > 0:
+                        cont = h.kind == "c"
+                        k_mlp_train(KIND_CONT if cont else KIND_CHOICE, h.actor, h.obs, h.ret, h.obs.new_empty(0),
+                                    h.act if (cont or h.per_row) else None, h.logp, stp,
+                                    None if (cont or h.per_row) else h.counts, m_global=h.m, sums=sa, exact=h.exact)
+                        trained.append(h.actor)
+                        out[i][0] = sums[H + i, 0:1]
+                    if crit:
+                        k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sc, exact=h.exact)
+                        trained.append(h.critic)
+                        out[i][1] = sums[i, 0:1]
+                    continue
+                if k > 0 and crit and paired[i]:
+                    _pair_pass(p, h, stp, sa, sc, st)
+                    trained += [h.actor, h.critic]
+                    out[i] = [sums[H + i, 0:1], sums[i, 0:1]]
+                    continue
+                if k > 0:  # the actor pass of epoch k - 1
+                    _actor_pass(p, h, stp, sa, st)
                     trained.append(h.actor)
                     out[i][0] = sums[H + i, 0:1]
-                if crit:
-                    k_mlp_train(KIND_CRITIC, h.critic, h.obs, h.ret, m_global=h.m, sums=sc, exact=h.exact)
+                if crit:  # the critic pass of epoch k
+                    _critic_pass(p, h, sc, st)
                     trained.append(h.critic)
                     out[i][1] = sums[i, 0:1]
-                continue
-            if k > 0 and crit and paired[i]:
-                _pair_pass(p, h, stp, sa, sc, st)
-                trained += [h.actor, h.critic]
-                out[i] = [sums[H + i, 0:1], sums[i, 0:1]]
-                continue
-            if k > 0:  # the actor pass of epoch k - 1
-                _actor_pass(p, h, stp, sa, st)
-                trained.append(h.actor)
-                out[i][0] = sums[H + i, 0:1]
-            if crit:  # the critic pass of epoch k
-                _critic_pass(p, h, sc, st)
-                trained.append(h.critic)
-                out[i][1] = sums[i, 0:1]
+        for sd in side:  # join
+            main.wait_stream(sd)
         if crit:
             stats = sums[:H, 1:3].reshape(-1).contiguous()
             _allreduce_(stats)
