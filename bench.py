@@ -6,7 +6,7 @@ Algo_PPO.train(1) (Coop-MH-PPO-scalable.py:854-917), reward-curve file writing o
     rollout.reset() -> reset N envs + 80 rollout steps (choice head at t=0; per step:
     policy kernel + fused sample/env-step kernel, two env halves on two streams; at small N
     one chain replayed from a HIP graph) -> returns scan -> bucketing -> 10 joint epochs of
-    the three heads (cross, wait, choice; the heads' passes alternate over two streams) ->
+    the three heads (cross, wait, choice) ->
     immediate rewards, the
     reward-sum all-reduce and its host read (the reward curves) -> rollout.reset().
 Default workload (BASELINE.json configs[2], the metric's "65536 envs x 4 agents"):
@@ -26,7 +26,8 @@ Extra JSON fields:
                  ~85 % of GPU time): algorithmic FLOPs per row x rows /
                  launch duration, from HIP events on its stream around each launch of one
                  extra training iteration run right after the timed region with the passes on
-                 one stream (concurrent launches on two streams would blur the events).  The kernel runs the bf16x3 split path
+                 one stream (the timed region carries no per-launch events; with
+                 MHPPO_TRAIN_STREAMS=2 its concurrent launches would blur them).  The kernel runs the bf16x3 split path
                  (six bf16 MFMAs per f32 product, f32-level accuracy), so its
                  ceiling is the bf16 dense MFMA peak / 6 = 419.4 TFLOP/s of f32-equivalent
                  work; the fraction of the f32-MFMA peak (157.3) is reported beside it.

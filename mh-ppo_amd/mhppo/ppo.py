@@ -428,8 +428,11 @@ def _pair_pass(p, h, stats, sums_a, sums_c, st):
 # stream i % TRAIN_STREAMS (a head's actor and critic passes stay in order on one stream: the critic
 # pass e + 1 overwrites the V_e the actor pass e reads).  The heads are independent within a step, so
 # one head's launch and weight staging overlap the other's tail, partial fold and reduction
-# (mhppo_mlp_train keeps a workspace per stream).  MHPPO_TRAIN_STREAMS=1: one stream (A/B).
-TRAIN_STREAMS = max(1, int(os.environ.get("MHPPO_TRAIN_STREAMS", "2")))
+# (mhppo_mlp_train keeps a workspace per stream).  Measured -0.7 % per iteration with two streams
+# (profiles/r04_streams/), but then each kernel's execution span (rocprofv3) includes the time its
+# blocks wait behind the other stream's kernel, so the per-kernel profile no longer matches the
+# kernel's own duration: the default stays one stream; MHPPO_TRAIN_STREAMS=2 opts in.
+TRAIN_STREAMS = max(1, int(os.environ.get("MHPPO_TRAIN_STREAMS", "1")))
 _SIDE_STREAMS = {}
 
 
