@@ -70,7 +70,8 @@ struct Lay {
                        O_WEND = (O_B4 + NOUT + 3) / 4 * 4;
   // per-wave input slot: X [32][n_in], s0 = [ret 32 | V 32], s1 = [act or logp_old 32 | logp_old 32]
   static constexpr int XMAX = PF ? 32 * NIN_CONT : 64 * KS;
-  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = IN_S0 + 64, IN_SZ = IN_S1 + 64;
+  // PF: 32 floats of pad after s1 take the unpredicated DMAs' overhang (prefetch_tile)
+  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = IN_S0 + 64, IN_SZ = IN_S1 + 64 + (PF ? 32 : 0);
   static constexpr int NSLOT = PF ? 2 : 1;
   // per-wave scratch: 3 transpose tiles, then the input slot(s)
   static constexpr int O_T = 0, O_IN = 3 * TILE, WAVE_LDS = O_IN + NSLOT * IN_SZ;
@@ -240,6 +241,7 @@ template <int KIND, class LY>
 __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const float *ret, const float *V,
                                               const float *act, const float *lp, int64_t row0, int l) {
   const v4i rx = rsrc_v(X + row0 * NIN_CONT, 32 * NIN_CONT * 4);
+#ifdef MHPPO_X3_DMA_PRED
   dma16(rx, slot + LY::IN_X, 16 * l);
   if (l < 40) dma16(rx, slot + LY::IN_X + 256, 1024 + 16 * l);
   const uint32_t vo = 4 * (l & 31);
@@ -249,6 +251,21 @@ __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const
     if (l < 32) dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);
     if (l >= 32) dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1, vo);
   }
+#else
+  // Every DMA on all 64 lanes (no exec-mask branches): an LDS-DMA lane writes base + 4 lane, so
+  // the lanes past a piece's end land in the NEXT piece's place (or the 32-float pad after s1),
+  // reading zeros past their buffer's bounds; the pieces are issued in address order and their
+  // LDS writes land in issue order, so each overhang is overwritten by the piece it covers.
+  dma16(rx, slot + LY::IN_X, 16 * l);
+  dma16(rx, slot + LY::IN_X + 256, 1024 + 16 * l);  // X 256..415; lanes 40-63: zeros into s0
+  const uint32_t vo = 4 * l;
+  dma4(rsrc_v(ret + row0, 128), slot + LY::IN_S0, vo);  // ret [0, 32); lanes 32-63: zeros [32, 64)
+  if (KIND == K_CONT) {
+    dma4(rsrc_v(V + row0, 128), slot + LY::IN_S0 + 32, vo);   // V [32, 64); overhang into s1
+    dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);      // act [0, 32); overhang [32, 64)
+    dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1 + 32, vo);  // logp_old [32, 64); overhang: pad
+  }
+#endif
 }
 template <int KIND>
 constexpr int prefetch_ops() { return KIND == K_CRITIC ? 3 : 6; }  // DMA instructions per prefetch
@@ -768,7 +785,7 @@ struct Geo {
   // input slot (floats): X [32][nin] | s0 [32 | 32] | s1 [32 | 32].  A runtime nin gets an X region
   // of whole 1-KiB pieces, so every LDS-DMA piece lands unmasked (zeros past the rows).
   static constexpr int XMAX = NIC ? (32 * NIC + 3) / 4 * 4 : (32 * (K1 - 1) + 255) / 256 * 256;
-  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = XMAX + 64, IN_SZ = XMAX + 128;
+  static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = XMAX + 64, IN_SZ = XMAX + 128 + (NIC ? 32 : 0);
   static constexpr int XPIECES = (XMAX * 4 + 1023) / 1024;
   static constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
   static constexpr int LDS_BYTES = NET_B + WAVES * WAVE_B;
