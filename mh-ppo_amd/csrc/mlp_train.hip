@@ -1825,6 +1825,7 @@ constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3
 #define MHPPO_X3_CRIT 13  // W2's forward fragments held, dW4 in registers, DH2F + XCE (ab_crit.txt)
 #endif
 constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
+constexpr int X3_CRIT_HB = 3 & ~((MHPPO_X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
 constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 #ifndef MHPPO_X3_ACT
 // the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
@@ -1864,7 +1865,8 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   constexpr bool A13 = KIND == K_CONT;
   constexpr bool CC = KIND == K_CRITIC && !C13, CA = KIND == K_CHOICE;  // the choice head's nets
   constexpr bool ORD = (A13 && X3_ACT_ORD) || (C13 && X3_CRIT_ORD) || (CC && X3_CC_ORD) || (CA && X3_CA_ORD);
-  Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : (CC ? X3_CC_HF : X3_CA_HF)), A13 ? X3_ACT_HB : 3, G,
+  Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : (CC ? X3_CC_HF : X3_CA_HF)),
+       A13 ? X3_ACT_HB : (C13 ? X3_CRIT_HB : 3), G,
        (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR), ORD, ORD,
        (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R) || (CC && X3_CC_W4R)>
       p;
