@@ -241,17 +241,6 @@ template <int KIND, class LY>
 __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const float *ret, const float *V,
                                               const float *act, const float *lp, int64_t row0, int l) {
   const v4i rx = rsrc_v(X + row0 * NIN_CONT, 32 * NIN_CONT * 4);
-#ifdef MHPPO_X3_DMA_PRED
-  dma16(rx, slot + LY::IN_X, 16 * l);
-  if (l < 40) dma16(rx, slot + LY::IN_X + 256, 1024 + 16 * l);
-  const uint32_t vo = 4 * (l & 31);
-  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + LY::IN_S0, vo);
-  if (KIND == K_CONT) {
-    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + LY::IN_S0, vo);
-    if (l < 32) dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);
-    if (l >= 32) dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1, vo);
-  }
-#else
   // Every DMA on all 64 lanes (no exec-mask branches): an LDS-DMA lane writes base + 4 lane, so
   // the lanes past a piece's end land in the NEXT piece's place (or the 32-float pad after s1),
   // reading zeros past their buffer's bounds; the pieces are issued in address order and their
@@ -265,7 +254,6 @@ __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const
     dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);      // act [0, 32); overhang [32, 64)
     dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1 + 32, vo);  // logp_old [32, 64); overhang: pad
   }
-#endif
 }
 template <int KIND>
 constexpr int prefetch_ops() { return KIND == K_CRITIC ? 3 : 6; }  // DMA instructions per prefetch
@@ -1015,10 +1003,6 @@ __device__ __forceinline__ void put_t(float *T, const f32x16 &v, int l) {
 #pragma unroll
   for (int r = 0; r < 16; r++) b[((r & 3) + 8 * (r >> 2)) * TS] = v[r];
 }
-#ifdef MHPPO_X3_PROBE_NOSUMS
-// A/B probe only (wrong bias gradients): what the per-tile LDS row sums cost
-#define X3_ROWSUM(k, v) radd(k, (v)[0] + (v)[5])
-#else
 #define X3_ROWSUM(k, v) \
   do {                   \
     put_t(T, v, l);      \
@@ -1026,7 +1010,6 @@ __device__ __forceinline__ void put_t(float *T, const f32x16 &v, int l) {
     radd(k, half_row_sum(T, l)); \
     lds_order();         \
   } while (0)
-#endif
 __device__ __forceinline__ float half_row_sum(const float *T, int l) {
   const float4 *p = reinterpret_cast<const float4 *>(T + (l & 31) * TS + 16 * (l >> 5));
   float s = 0.0f;
@@ -1334,17 +1317,12 @@ struct Pass {
         if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 128), 4 * j, 0, 0);
         const float a = rt - v;
         const float d = v - rt;
-#ifdef MHPPO_X3_PROBE_NOLOSS
-        dy0 = d * (float)inv_m;  // A/B probe only: no float64 loss / advantage sums
-        dsum0 += a;
-#else
         if (kh == 0) {
           dsum0 += (double)d * (double)d;
           dsum1 += (double)a;
           dsum2 += (double)a * (double)a;
         }
         dy0 = (float)(2.0 * inv_m * (double)d);
-#endif
       } else if constexpr (KIND == K_CONT) {
         const float t = tanhf(y0);
         const float mu = t * out_std + out_mean;
@@ -1353,17 +1331,11 @@ struct Pass {
         const float diff = (float)((double)slot[G::IN_S1 + j] - (double)mu);
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-#ifdef MHPPO_X3_PROBE_NOLOSS
-        const float rf = __expf(lp - slot[G::IN_S1 + 32 + j]);  // A/B probe only: float ratio
-        dsum0 += rf * A;
-        const float dmu = (float)inv_m * rf * A * x * MVN_INV_L;
-#else
         const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
         double dfdr;
         const double f = surr_and_grad(r, (double)A, dfdr);
         if (kh == 0) dsum0 += f;
         const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
-#endif
         dy0 = (dmu * out_std) * (1.0f - t * t);
       } else {
         // choice actor (train_model_d :818-851): softmax over the pair (as torch: shift by the
@@ -1420,11 +1392,7 @@ struct Pass {
         for (int r = 0; r < 16; r++) gW4r1[r] += dy1 * h3[r];
       }
     } else {
-#ifdef MHPPO_X3_PROBE_NOW4
-      radd(3, g[0]);  // A/B probe only: the dW4 row sum removed (wrong dW4)
-#else
       X3_ROWSUM(3, g);
-#endif
       if constexpr (NOUT == 2) {
         f32x16 g1;
 #pragma unroll
@@ -1774,12 +1742,7 @@ __device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int
     const int nrows = (int)min((int64_t)32, M - row0);
     float *slot = ws.inb + cb * G::IN_SZ;
     const int64_t nxt = tile + nw;
-#ifdef MHPPO_X3_PROBE_NODMA
-    cb = 0;  // A/B probe only: every tile reuses the first tile's inputs (no DMA after it)
-    if (false) {
-#else
     if (nxt < nfull) {
-#endif
       prefetch(ws.inb + (cb ^ 1) * G::IN_SZ, nxt * 32);
       if constexpr (FIXED) wait_vmcnt<prefetch_ops<KIND>()>();
       else wait_vmcnt<prefetch_g_ops<KIND, G>()>();
@@ -1891,10 +1854,6 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
 // two.  The actor reads V_e from the tile's prefetched inputs before the critic overwrites those
 // rows of V with V_{e+1} (each tile belongs to one wave; its inputs land one tile ahead).
 // Partials: actor at gpart[gw], critic at gpart[nw + gw] (and dpart likewise).
-#ifndef MHPPO_PAIR_HB
-#define MHPPO_PAIR_HB 0
-#endif
-constexpr int PAIR_HB = MHPPO_PAIR_HB;
 __global__ void __launch_bounds__(64 * x3::WAVES)
     k_mlp_train_x3_pair(const float *__restrict__ Wa, const float *__restrict__ Wc, const float *__restrict__ X,
                         int64_t M, const float *__restrict__ ret, float *__restrict__ V,
@@ -1913,8 +1872,8 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   stage_net<G>(Wa, L8, tid, NIN_CONT);
   stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
-  Pass<K_CONT, false, PAIR_HB, G, X3_BS_PAIR, true> pa;
-  Pass<K_CRITIC, false, PAIR_HB, G, X3_BS_PAIR, true> pc;
+  Pass<K_CONT, false, 0, G, X3_BS_PAIR, true> pa;  // two nets in one wave: no fragments held
+  Pass<K_CRITIC, false, 0, G, X3_BS_PAIR, true> pc;
   pa.init(L8, ws);
   pc.init(L8 + G::NET_B, ws);
   float meanf, stdf;

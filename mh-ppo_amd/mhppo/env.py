@@ -155,8 +155,22 @@ class VecCrosswalk:
         _lib.check(L.mhppo_env_export(self._h, _lib.ptr(blob), _lib.stream_ptr(device=self.device)))
         return {"cfg": self._cfg_key(), "layout": self.STATE_LAYOUT, "blob": blob.cpu()}
 
+    @staticmethod
+    def blob_layout(sd, state_bytes=None):
+        """The layout version of an exported blob.  Checkpoints written before the key existed
+        (r02 and r03) carry none: an r03 blob is layout 2 and has the layout-2 size (four MT blocks
+        per env), an r02 blob is smaller (two), so a key-less blob of the size this build's layout 2
+        exports (`state_bytes`) is layout 2 and any other key-less blob layout 1."""
+        if "layout" in sd:
+            return int(sd["layout"])
+        blob = sd.get("blob")
+        if blob is not None and state_bytes is not None and int(blob.numel()) == int(state_bytes):
+            return 2
+        return 1
+
     def load_state_dict(self, sd):
-        lay = int(sd.get("layout", 1))
+        n = None if "layout" in sd or self.STATE_LAYOUT != 2 else int(_lib.lib().mhppo_env_state_bytes(self._h))
+        lay = VecCrosswalk.blob_layout(sd, n)
         if lay != self.STATE_LAYOUT:
             raise ValueError(f"env checkpoint has state layout {lay}, this build reads layout {self.STATE_LAYOUT} "
                              "(the blob layout changed between versions; it cannot be converted)")

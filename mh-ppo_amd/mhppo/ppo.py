@@ -547,11 +547,14 @@ class _AdamPlan:
 
     def __init__(self, opts, keys, groups, steps, grads):
         self.opts, self.keys, self.groups, self.steps = opts, keys, groups, steps
-        self.ids = [(id(o.state), id(o.param_groups)) for o in opts]
+        # strong references, compared by identity: an id() of a state dict freed by a later
+        # load_state_dict could be reused by a newer one and pass a stale plan
+        self.refs = [(o.state, o.param_groups) for o in opts]
         self.grads = grads  # [(param, grad)]
 
     def valid(self, opts):
-        if [(id(o.state), id(o.param_groups)) for o in opts] != self.ids:
+        if len(opts) != len(self.refs) or not all(o.state is st and o.param_groups is pg
+                                                  for o, (st, pg) in zip(opts, self.refs)):
             return False
         if _group_keys(opts) != self.keys or not all(_no_step_hooks(o) for o in opts):
             return False

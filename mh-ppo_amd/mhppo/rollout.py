@@ -114,6 +114,7 @@ class RolloutGPU:
         self._bufs = b
         # captured one-chain step loops, keyed by what their launches bake in (collect)
         self._graphs = {}
+        self._cap_stream = None  # the graph capture stream, on the env's device (created at first capture)
         self.use_graph = default_graph() if dev.type == "cuda" else 0
         # parts > 1: part p > 0 steps on its own stream (created once), part 0 on the caller's
         self._side = [torch.cuda.Stream(device=dev) for _ in range(self.parts - 1)] if dev.type == "cuda" else []
@@ -255,20 +256,29 @@ class RolloutGPU:
             # actors' mean / std are baked into the graph's nodes and key it), without the
             # per-launch host work — which at small N is the step's time, and at large N keeps the
             # host from queueing the bucketing until the rollout has nearly finished.
+            # Capture and replay with the env's device current and on a capture stream OF that
+            # device: torch.cuda.graph's default capture stream is created once, on whichever
+            # device was current at its first use, and a launch on another device's stream would
+            # run eagerly outside the capture (an empty graph, replayed silently).  The replay
+            # goes to dev's current stream, ordered after mhppo_rollout_begin above.
             key = (fused, nparts, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
-            g = self._graphs.get(key)
-            if g is None:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    cap = torch.cuda.current_stream(dev)
-                    if fused or nparts == 1:
-                        self._step_loop(L, mx, mw, fused, cap.cuda_stream, None)
-                    else:
-                        self._parts_loop(L, mx, mw, nparts, cap)
-                if len(self._graphs) > 8:
-                    self._graphs.clear()
-                self._graphs[key] = g
-            g.replay()
+            with torch.cuda.device(dev):
+                g = self._graphs.get(key)
+                if g is None:
+                    if self._cap_stream is None:
+                        self._cap_stream = torch.cuda.Stream(device=dev)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=self._cap_stream):
+                        cap = torch.cuda.current_stream(dev)
+                        assert cap == self._cap_stream, "graph capture must run on the env's device"
+                        if fused or nparts == 1:
+                            self._step_loop(L, mx, mw, fused, cap.cuda_stream, None)
+                        else:
+                            self._parts_loop(L, mx, mw, nparts, cap)
+                    if len(self._graphs) > 8:
+                        self._graphs.clear()
+                    self._graphs[key] = g
+                g.replay()
         elif fused or nparts == 1:
             self._step_loop(L, mx, mw, fused, st, step_events)
         else:
@@ -350,12 +360,17 @@ def bucket_segments(batch, fix_bucket=False, status=None):
     # room for every segment; the choice batch gathered over all segment slots (existing ones
     # first: nonzero_static pads with slot 0); the choice action counts.  After the sync the
     # batches are leading views of those buffers.
+    # Both buckets share ONE buffer of NS + 3 segments (not one of NS each: that doubled the
+    # bucketing's peak memory): cross segments from slot 0, wait segments from slot w0 = the cross
+    # count rounded up to a multiple of 4, computed on the device, so the wait bucket's observation
+    # rows start 16-byte aligned at any T (the train kernels' LDS-DMA rows; 4 T 52 B = 16 T 13 B).
     ret = returns_scan_tm(batch.rew_tm)  # [T, N, S]
     cc, cw = torch.cumsum(cross, 0), torch.cumsum(wait, 0)
-    pos = torch.where(cross, cc - 1, torch.where(wait, cw - 1, -1))
-    bucket = wait.to(torch.int8)
-    cross_r, wait_r = scatter_positions(pos, bucket, (NS, NS), NS, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm,
-                                        ret, batch.rew_tm)
+    w0 = torch.div(cc[-1] + 3, 4, rounding_mode="floor") * 4
+    pos = torch.where(cross, cc - 1, torch.where(wait, w0 + cw - 1, -1))
+    bucket = torch.zeros(NS, dtype=torch.int8, device=pos.device)
+    (both,) = scatter_positions(pos, bucket, (NS + 3,), NS, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm, ret,
+                                batch.rew_tm)
     seg_all = torch.nonzero_static(exist, size=NS, fill_value=0).squeeze(1)
     cl = batch.closest.reshape(NS).long().index_select(0, seg_all)
     base = seg_all * P + cl
@@ -378,10 +393,10 @@ def bucket_segments(batch, fix_bucket=False, status=None):
             status.zero_()
         raise_if_nan_status(sizes[3])
     n_cross, n_wait, n_all = sizes[:3]
-    for o, n in ((cross_r, n_cross), (wait_r, n_wait)):
-        for k in ("obs", "act", "logp", "ret", "rew"):
-            o[k] = o[k][:n * T]
-        o["n_seg"] = n
+    c0 = (n_cross + 3) // 4 * 4  # = w0
+    cross_r = {k: both[k][:n_cross * T] for k in ("obs", "act", "logp", "ret", "rew")}
+    wait_r = {k: both[k][c0 * T:(c0 + n_wait) * T] for k in ("obs", "act", "logp", "ret", "rew")}
+    cross_r["n_seg"], wait_r["n_seg"] = n_cross, n_wait
     choice = {k: v[:n_all] for k, v in choice.items()}
     choice["n_seg"] = n_all
     choice["counts"] = counts  # float64 [2] on the device: (act == 0).sum(), (act == 1).sum()
@@ -405,7 +420,7 @@ def scatter_positions(pos, bucket, sizes, NS, T, obs_tm, act_tm, logp_tm, ret_tm
     """scatter_buckets with the segments given as positions: segment s goes to row block pos[s]
     of bucket bucket[s] (pos < 0: no bucket); sizes = the two buckets' segment counts."""
     dev = obs_tm.device
-    outs, dst = [], (_lib.BucketDst * 2)()
+    outs, dst = [], (_lib.BucketDst * 2)()  # one size: bucket 1 unused (every bucket[s] = 0)
     for b, n in enumerate(sizes):
         o = dict(obs=torch.empty(n * T, NF_C, dtype=torch.float32, device=dev),
                  act=torch.empty(n * T, dtype=torch.float32, device=dev),

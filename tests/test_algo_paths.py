@@ -42,9 +42,20 @@ def test_env_checkpoint_layout_version_is_checked():
 
         def _cfg_key(self):
             return [0]
-    for old in ({"cfg": [0], "blob": None}, {"cfg": [0], "layout": VecCrosswalk.STATE_LAYOUT - 1, "blob": None}):
+    for old in ({"cfg": [0], "layout": VecCrosswalk.STATE_LAYOUT - 1, "blob": None},):
         with pytest.raises(ValueError, match="state layout"):
             VecCrosswalk.load_state_dict(_E(), old)
+
+
+def test_env_checkpoint_keyless_layout_inferred_from_size():
+    # r02 / r03 checkpoints carry no "layout" key: an r03 blob has the layout-2 size, an r02 blob not
+    import torch
+    from mhppo.env import VecCrosswalk
+    blob = torch.zeros(1000, dtype=torch.uint8)
+    assert VecCrosswalk.blob_layout({"cfg": [0], "blob": blob}, 1000) == 2
+    assert VecCrosswalk.blob_layout({"cfg": [0], "blob": blob}, 1200) == 1
+    assert VecCrosswalk.blob_layout({"cfg": [0], "blob": None}, 1000) == 1
+    assert VecCrosswalk.blob_layout({"cfg": [0], "layout": 7, "blob": blob}, 1000) == 7
 
 
 def test_curves_flush_pending_entries():

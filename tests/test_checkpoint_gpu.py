@@ -39,3 +39,17 @@ def test_resume_is_bit_identical(tmp_path, monkeypatch):
     assert torch.equal(ref[2], got[2]) and torch.equal(ref[3], got[3])
     assert ref[4] == got[4] and ref[5] == got[5] == 3
     assert (tmp_path / "load_model" / "parameters").is_dir()  # train() wrote the reward curves (:908-916)
+
+
+def test_keyless_env_checkpoint_loads_as_layout_2():
+    # an r03 env checkpoint has no "layout" key; its blob is layout 2: it must resume
+    from mhppo.env import VecCrosswalk
+    v = VecCrosswalk("coop", 128, 2, 1, 2, seed_base=5)
+    v.reset()
+    v.step(torch.zeros(128, 2 * v.n_slots, device=v.device))
+    sd = v.state_dict()
+    del sd["layout"]
+    w = VecCrosswalk("coop", 128, 2, 1, 2, seed_base=5)
+    w.load_state_dict(sd)
+    assert torch.equal(v.get_rng()[0], w.get_rng()[0]) and torch.equal(v.get_rng()[1], w.get_rng()[1])
+    assert torch.equal(v.get_state(), w.get_state())

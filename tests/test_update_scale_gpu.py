@@ -132,18 +132,27 @@ def test_pair_launch_bit_identical_to_two_passes():
         _pair_vs_passes(algo.critic_net_cross, algo.actor_net_cross, obs[:n], ret[:n], act[:n], lp[:n], float(n))
 
 
-def test_pipelined_epochs_equal_sequential():
-    """Algo_PPO.update's pipelined epochs (ppo.train_epochs: actor e fused with critic e + 1) train
-    bit-identical nets to the epoch-by-epoch schedule (PIPELINE_PAIRS off: every pass its own
-    launch, the same order of Adam steps per optimiser)."""
+def test_pipelined_epochs_equal_sequential(monkeypatch):
+    """Algo_PPO.update's pipelined epochs (ppo.train_epochs: actor e fused with critic e + 1, or
+    with PIPELINE_PAIRS off every pass its own launch in the pipelined order) train bit-identical
+    nets to the schedule they replace: ten ppo.train_epoch calls (critic passes -> advantage sums
+    -> actor passes -> gradient all-reduce -> Adam, epoch by epoch)."""
     from mhppo import ppo
     from mhppo.algo import Algo_PPO
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
+    pipelined = ppo.train_epochs
+
+    def sequential(heads, n_epochs, bucket=None):
+        out = None
+        for _ in range(n_epochs):
+            out = ppo.train_epoch(heads, bucket)
+        return out
     nets = []
     try:
-        for pipe in (True, False):
-            ppo.PIPELINE_PAIRS = pipe
+        for arm in ("pairs", "no_pairs", "train_epoch"):
+            ppo.PIPELINE_PAIRS = arm == "pairs"
+            monkeypatch.setattr(ppo, "train_epochs", sequential if arm == "train_epoch" else pipelined)
             venv = VecCrosswalk("4cars", 2048, 4, 1, 2, seed_base=5)
             torch.manual_seed(0)
             algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=1, save_curves=False)
@@ -151,4 +160,5 @@ def test_pipelined_epochs_equal_sequential():
             nets.append(torch.cat([n.flat() for n in algo.nets()]).cpu())
     finally:
         ppo.PIPELINE_PAIRS = None
-    assert torch.equal(nets[0], nets[1])
+    assert torch.equal(nets[0], nets[2]), "pipelined (pairs) vs ten train_epoch calls"
+    assert torch.equal(nets[1], nets[2]), "pipelined (no pairs) vs ten train_epoch calls"
