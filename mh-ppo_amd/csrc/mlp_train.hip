@@ -38,6 +38,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/mhppo.h"
 #include "common.h"
@@ -990,6 +991,22 @@ __device__ __forceinline__ void img_write(char *wbase, const F3 &f0, const F3 &f
       *reinterpret_cast<uint2 *>(wbase + pt * PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
   }
 }
+// one part (hi / mid / lo) of img_write: two 16-byte row stores per lane (the hand-placed passes
+// spread an image's parts over MFMA shadows: at most two LDS stores or three reads per shadow keep
+// the LDS pipe from stalling the issue, MI355X_MICROARCH.md §LDS)
+__device__ __forceinline__ void img_write_pt(char *wbase, const F3 &f0, const F3 &f1, int pt) {
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const F3 &f = g < 2 ? f0 : f1;
+    const int q = 2 * (g & 1);
+    *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
+  }
+}
+// one part of a transposed fragment read (tr_pair): two ds_read_b64_tr_b16
+__device__ __forceinline__ void tr_pt(const char *p, int du, int pt, F3 &f) {
+  const uint2 a = tr16(p + pt * IM_PART), b = tr16(p + pt * IM_PART + du);
+  f.p[pt] = u32x4{a.x, a.y, b.x, b.y};
+}
 // K-step s (rows 16s .. 16s+15) of the image read transposed: lane (feature l & 31, half h)
 // gets rows 16s + 8h + j, j = 0..7; lane 4q + p of group G addresses row 16s + 8(G>>1) +
 // 4u + q, chunk 4(G&1) + p (rbase = img + (8 (G>>1) + q) * IM_ROWB + 8 (4 (G&1) + p)).
@@ -1038,6 +1055,109 @@ __device__ __forceinline__ void stage_w(char *Wimg, int part, int rowb, int row,
 __device__ __forceinline__ void relu_mask(f32x16 &d, const f32x16 &h) {
 #pragma unroll
   for (int r = 0; r < 16; r++) d[r] = h[r] > 0.0f ? d[r] : 0.0f;
+}
+}  // namespace x3
+
+namespace x3 {
+// ---- Hand-placed backward (SCH passes): each block of MFMAs carries the NEXT block's VALU / LDS
+// work in its MFMA shadows.  One wave per SIMD issues in order: a run of back-to-back MFMAs leaves
+// the vector issue idle for 24 of every 32 cycles, a run of VALU leaves the matrix pipe idle, and
+// the compiler cannot place VALU between the MFMAs of an opaque inline-asm block.  So every MFMA
+// is its own statement and `weave` cuts the block into regions (sched_barrier: nothing crosses),
+// region k = MFMA k + a share of the payload units, spread evenly (unit u in region u NMU / NU).
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+// A payload plan: segments {first region, end region, units}, the units numbered in segment order
+// and spread evenly over their segment's regions (unit t of a segment in r0 + t (r1 - r0) / n).
+template <int... S>
+struct Plan {
+  static constexpr int NS = sizeof...(S) / 3;
+  static constexpr int s[sizeof...(S)] = {S...};
+  static constexpr int units() {
+    int n = 0;
+    for (int i = 0; i < NS; i++) n += s[3 * i + 2];
+    return n;
+  }
+  static constexpr int NU = units();
+  static constexpr int reg(int u) {  // the region of unit u
+    for (int i = 0; i < NS; i++) {
+      const int n = s[3 * i + 2];
+      if (u < n) return s[3 * i] + u * (s[3 * i + 1] - s[3 * i]) / n;
+      u -= n;
+    }
+    return -1;
+  }
+  static constexpr int first(int seg) {  // the first unit of segment seg
+    int n = 0;
+    for (int i = 0; i < seg; i++) n += s[3 * i + 2];
+    return n;
+  }
+  static_assert(sizeof...(S) % 3 == 0, "plan: {r0, r1, units} triples");
+};
+// region k = MFMA k (mf(k)), then the payload units the plan puts in region k; nothing crosses a
+// region border (sched_barrier)
+template <int NM, class PL, class M, class U>
+__device__ __forceinline__ void weave(M &&mf, U &&un) {
+  static_assert(PL::NU == 0 || PL::reg(PL::NU - 1) < NM, "plan: units past the block's last region");
+  sfor<0, NM>([&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    mf(kc);
+    sfor<0, PL::NU>([&](auto uc) {
+      if constexpr (PL::reg(decltype(uc)::value) == K) un(uc);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+// the six products of a split x split MFMA (mfma6 order, smallest first) and the three of a
+// split x one-hot one (macc3)
+constexpr int P6A[6] = {2, 0, 1, 1, 0, 0}, P6B[6] = {0, 2, 1, 0, 1, 0};
+// one weight-gradient MFMA, accumulator in AGPRs (volatile: kept in its region).  Its A / B come
+// from LDS reads (or loop-invariant registers), never from a VALU write just before it: no wait
+// states needed (tools/check_asm_rd.py checks the built code)
+__device__ __forceinline__ void mac1(const u32x4 &a, const u32x4 &b, f32x16 &c) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// the bias-sum MFMA: B = a loop-invariant one-hot fragment, kept in AGPRs (an MFMA reads A / B from
+// either file; as "v" the compiler would copy it from the AGPR it parks it in right before the MFMA,
+// a VALU write the MFMA then reads without its two wait states)
+__device__ __forceinline__ void mac1_oh(const u32x4 &a, const u32x4 &oh, f32x16 &c) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "a"(oh));
+}
+__device__ __forceinline__ void mac1_16(const u32x4 &a, const u32x4 &b, f32x4 &c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// The regions hold because the train translation unit is built with the source-order SelectionDAG
+// scheduler (csrc/Makefile: -pre-RA-sched=source): instruction selection keeps each payload unit
+// where the source puts it, and the machine scheduler never moves an instruction across a region
+// barrier.  (Pinning the units with empty volatile asm statements instead cost one copy and one
+// wait state per pinned value.)
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+// split level 1 of element pair q of an 8-element fragment v: hi part, residuals r[2q], r[2q+1]
+__device__ __forceinline__ void split_l1(const float *v, int q, F3 &f, float *r) {
+  const uint32_t h = pk_bf16(v[2 * q], v[2 * q + 1]);
+  f.p[0][q] = h;
+  r[2 * q] = v[2 * q] - __uint_as_float(h << 16);
+  r[2 * q + 1] = v[2 * q + 1] - __uint_as_float(h & 0xffff0000u);
+}
+// split levels 2-3 of pair q from its residuals (as split_pair: the same bits)
+__device__ __forceinline__ void split_l2(int q, F3 &f, const float *r) {
+  const uint32_t m = pk_bf16(r[2 * q], r[2 * q + 1]);
+  f.p[1][q] = m;
+  f.p[2][q] = pk_bf16(r[2 * q] - __uint_as_float(m << 16), r[2 * q + 1] - __uint_as_float(m & 0xffff0000u));
+}
+// ReLU-derivative mask of elements r, r + 1 of d by h > 0
+__device__ __forceinline__ void mask2(f32x16 &d, const f32x16 &h, int r) {
+  d[r] = h[r] > 0.0f ? d[r] : 0.0f;
+  d[r + 1] = h[r + 1] > 0.0f ? d[r + 1] : 0.0f;
+}
+__device__ __forceinline__ void relu4(f32x16 &h, int r0) {
+#pragma unroll
+  for (int r = r0; r < r0 + 4; r++) h[r] = relu_bits(h[r]);
 }
 }  // namespace x3
 
@@ -1145,8 +1265,9 @@ constexpr bool X3_W4R = MHPPO_X3_W4R;
 // shadow); XCE: dW1's first input-column split issued before the dH1 MFMAs.  Measured per kernel
 // (profiles/r04_x3_bs/ab_order.txt): continuous actor both (-1.9 %), fused pair DH2F (-1.6 %), the
 // critic neither (its 512 registers: +3 % with either).
+// SCH: the hand-placed backward (bwd_s) — the 13-input heads' single-net passes.
 template <int KIND, int HF, int HB, class G, bool BS = false, bool DH2F = false, bool XCE = false,
-          bool W4R_ = KIND == K_CONT>
+          bool W4R_ = KIND == K_CONT, bool SCH = false>
 struct Pass {
   static constexpr int KS1 = G::KS1, NOUT = G::NOUT;
   static_assert(NOUT == (KIND == K_CHOICE ? 2 : 1), "outputs");
@@ -1274,22 +1395,27 @@ struct Pass {
     MHPPO_MARK(2);
     // ---- layer 2 (the biases ride in as the chains' initial accumulators)
     f32x16 h2a = feat_vec(F, kh), h2b = feat_vec(F + 32, kh);
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const F3 b = split_step(h1, s);
-      h2a = mfma6(fw2(0, s), b, h2a);
-      h2b = mfma6(fw2(1, s), b, h2b);
-    }
-    relu16(h2a);
-    relu16(h2b);
-    x3_phase();
-    MHPPO_MARK(3);
-    // ---- layer 3
     f32x16 h3 = feat_vec(F + 64, kh);
+    F3 h1s[2], h2as[2], h2bs[2], xb;  // SCH: the forward's splits (kept for the backward's images)
+    if constexpr (SCH) {
+      fwd_s(ws, Xs, h1, h1s, h2a, h2b, h2as, h2bs, h3, xb);
+    } else {
 #pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(s), split_step(h2a, s), h3);
+      for (int s = 0; s < 2; s++) {
+        const F3 b = split_step(h1, s);
+        h2a = mfma6(fw2(0, s), b, h2a);
+        h2b = mfma6(fw2(1, s), b, h2b);
+      }
+      relu16(h2a);
+      relu16(h2b);
+      x3_phase();
+      MHPPO_MARK(3);
+      // ---- layer 3
 #pragma unroll
-    for (int s = 0; s < 2; s++) h3 = mfma6(fw3(2 + s), split_step(h2b, s), h3);
+      for (int s = 0; s < 2; s++) h3 = mfma6(fw3(s), split_step(h2a, s), h3);
+#pragma unroll
+      for (int s = 0; s < 2; s++) h3 = mfma6(fw3(2 + s), split_step(h2b, s), h3);
+    }
     relu16(h3);
     x3_phase();
     MHPPO_MARK(4);
@@ -1376,6 +1502,10 @@ struct Pass {
     }
     radd(4, (kh == 0) ? dy0 : 0.0f);
     if constexpr (NOUT == 2) radd(6, (kh == 0) ? dy1 : 0.0f);
+    if constexpr (SCH) {
+      bwd_s(ws, h1, h1s, h2a, h2b, h2as, h2bs, h3, w4v, dy0, xb);
+      return;
+    }
     // ---- layer 4 backward: d3 = dH3^T masked; dW4 = row sums of dy h3; dB3 = row sums of d3
     f32x16 g, d3;
 #pragma unroll
@@ -1386,7 +1516,7 @@ struct Pass {
     }
     if constexpr (W4R) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) gW4r[r] += g[r];
+      for (int r = 0; r < 16; r++) gW4r[r] = fmaf(dy0, h3[r], gW4r[r]);
       if constexpr (NOUT == 2) {
 #pragma unroll
         for (int r = 0; r < 16; r++) gW4r1[r] += dy1 * h3[r];
@@ -1562,6 +1692,332 @@ struct Pass {
     lds_order();
     x3_phase();
     MHPPO_MARK(9);
+  }
+
+  // Layers 2 and 3 of one tile, hand-placed (SCH): each layer's MFMAs carry the splits its own later
+  // K-steps and the next layer need (the same products in the same order per accumulator as the
+  // plain forward, so the same bits):
+  //   L2  [h2a s0 | h2a s1 | h2b s0 | h2b s1]  | h1's K-step 1 split, dW1's input-column split,
+  //                                              h2a's ReLU and split (after its last MFMA)
+  //   L3  [h2a s0 | h2a s1 | h2b s0 | h2b s1]  | the rest of h2a's split, h2b's ReLU and split
+  // h1 arrives ReLU'd; h2a / h2b / h3 leave as the layers' pre-ReLU accumulators for h3 (the caller
+  // applies its ReLU) and ReLU'd for h2a / h2b.
+  __device__ __forceinline__ void fwd_s(const WaveSlot<G> &ws, const float *Xs, const f32x16 &h1, F3 (&h1s)[2],
+                                        f32x16 &h2a, f32x16 &h2b, F3 (&h2as)[2], F3 (&h2bs)[2], f32x16 &h3,
+                                        F3 &xb) {
+    const int l = ws.l, G_ = ws.G;
+    float rs[8], rt[8], xv[8];
+    float h1v[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) h1v[r] = h1[r];
+#pragma unroll
+    for (int q = 0; q < 4; q++) split_l1(h1v, q, h1s[0], rs);
+#pragma unroll
+    for (int q = 0; q < 4; q++) split_l2(q, h1s[0], rs);
+    {
+      const F3 w00 = fw2(0, 0), w01 = fw2(0, 1), w10 = fw2(1, 0), w11 = fw2(1, 1);
+      // h1 s1 split (8 units, before k = 6), dW1's B operand (1 + 8), h2a ReLU (4, after its last
+      // MFMA k = 11 has landed) + h2a s0 split (8) + h2a s1 split level 1 (4)
+      using PL = Plan<0, 5, 8, 5, 12, 10, 13, 24, 16>;
+      static_assert(PL::reg(7) < 6, "h1's K-step 1 before its MFMAs");
+      weave<24, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) h2a = mfma_b(w00.p[P6A[P]], h1s[0].p[P6B[P]], h2a);
+            if constexpr (T == 1) h2a = mfma_b(w01.p[P6A[P]], h1s[1].p[P6B[P]], h2a);
+            if constexpr (T == 2) h2b = mfma_b(w10.p[P6A[P]], h1s[0].p[P6B[P]], h2b);
+            if constexpr (T == 3) h2b = mfma_b(w11.p[P6A[P]], h1s[1].p[P6B[P]], h2b);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            if constexpr (U < 8) {
+              if constexpr (U % 2 == 0) split_l1(h1v + 8, U / 2, h1s[1], rs);
+              else split_l2(U / 2, h1s[1], rs);
+            } else if constexpr (U < 10) {  // dW1's B operand: rows 8G .. 8G + 7 of input column l & 15
+              const int n = l & 15, nc = n < NIN_CONT ? n : NIN_CONT - 1;
+#pragma unroll
+              for (int q = 4 * (U - 8); q < 4 * (U - 7); q++) {
+                float v = Xs[(8 * G_ + q) * NIN_CONT + nc];
+                pin(v);  // an unconditional load (a select, not a branch around it)
+                xv[q] = n < NIN_CONT ? v : (n == NIN_CONT ? 1.0f : 0.0f);
+              }
+            } else if constexpr (U < 18) {
+              constexpr int V = U - 10;
+              if constexpr (V % 2 == 0) split_l1(xv, V / 2, xb, rt);
+              else split_l2(V / 2, xb, rt);
+            } else if constexpr (U < 22) {  // h2a's ReLU
+              relu4(h2a, 4 * (U - 18));
+            } else if constexpr (U < 30) {  // h2a K-step 0 split
+              constexpr int V = U - 22;
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = h2a[e];
+              if constexpr (V % 2 == 0) split_l1(v, V / 2, h2as[0], rs);
+              else split_l2(V / 2, h2as[0], rs);
+            } else {  // h2a K-step 1 split, level 1 (level 2 in L3)
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = h2a[8 + e];
+              split_l1(v, U - 30, h2as[1], rt);
+            }
+          });
+    }
+    MHPPO_MARK(3);
+    {
+      const F3 w0 = fw3(0), w1 = fw3(1), w2 = fw3(2), w3 = fw3(3);
+      // h2a s1 level 2 (4, before k = 6) + h2b ReLU 0-7 (2) + h2b s0 level 1 (4); h2b s0 level 2 (4,
+      // before k = 12) + h2b ReLU 8-15 (2) + h2b s1 level 1 (4); h2b s1 level 2 (4, before k = 18)
+      using PL = Plan<0, 6, 10, 6, 12, 10, 12, 18, 4>;
+      static_assert(PL::reg(3) < 6 && PL::reg(13) < 12 && PL::reg(23) < 18, "splits before their MFMAs");
+      weave<24, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) h3 = mfma_b(w0.p[P6A[P]], h2as[0].p[P6B[P]], h3);
+            if constexpr (T == 1) h3 = mfma_b(w1.p[P6A[P]], h2as[1].p[P6B[P]], h3);
+            if constexpr (T == 2) h3 = mfma_b(w2.p[P6A[P]], h2bs[0].p[P6B[P]], h3);
+            if constexpr (T == 3) h3 = mfma_b(w3.p[P6A[P]], h2bs[1].p[P6B[P]], h3);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            if constexpr (U < 4) {
+              split_l2(U, h2as[1], rt);
+            } else if constexpr (U < 6) {  // h2b's ReLU, elements 0-7
+              relu4(h2b, 4 * (U - 4));
+            } else if constexpr (U < 10) {
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = h2b[e];
+              split_l1(v, U - 6, h2bs[0], rs);
+            } else if constexpr (U < 14) {
+              split_l2(U - 10, h2bs[0], rs);
+            } else if constexpr (U < 16) {  // h2b's ReLU, elements 8-15
+              relu4(h2b, 8 + 4 * (U - 14));
+            } else if constexpr (U < 20) {
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = h2b[8 + e];
+              split_l1(v, U - 16, h2bs[1], rt);
+            } else {
+              split_l2(U - 20, h2bs[1], rt);
+            }
+          });
+    }
+  }
+
+  // The backward of one tile, hand-placed (SCH): five MFMA blocks, each carrying the work the
+  // next block needs in its MFMA shadows (the plans below place it; an image's stores and reads go
+  // one part (hi / mid / lo) per unit, at most two stores or two reads in a shadow):
+  //   A  dH2 = W3^T d3      24 on-chain MFMAs | d3's K-step-1 split, the d3 / h2a / h2b images and
+  //                                             their reads, dW4 sums
+  //   B  dW3 (+ dB3)        30 AGPR MFMAs     | the h2b image reads, d2a / d2b masks, d2a's split
+  //   C  dH1 = W2^T d2      24 on-chain MFMAs | d2b's split, the h1 / d2a images and their reads
+  //   D  dW2 (+ dB2)        36 AGPR MFMAs     | the d2 image reads, d1's mask and split, d1's image
+  //                                             and dW1's operand reads
+  //   E  dW1 (+ dB1)        12 AGPR MFMAs (16x16x32)
+  // The same products in the same order per accumulator as the phase-by-phase backward (the same
+  // bits); an image slot is rewritten only after its last reads were issued (a wave's LDS
+  // operations execute in order).  h1s / h2as / h2bs: the forward's splits (the image data);
+  // xb: dW1's B operand (input columns), split in the forward.
+  __device__ __forceinline__ void bwd_s(const WaveSlot<G> &ws, const f32x16 &h1, const F3 (&h1s)[2], const f32x16 &h2a,
+                                        const f32x16 &h2b, const F3 (&h2as)[2], const F3 (&h2bs)[2],
+                                        const f32x16 &h3, const f32x16 &w4v, float dy0, const F3 &xb) {
+    static_assert(KS1 == 1 && NOUT == 1 && BS && W4R && G::NIC == NIN_CONT, "SCH: the 13-input single-net passes");
+    char *imw = ws.imw;
+    const char *imr = ws.imr, *imr16 = ws.imr16;
+    constexpr int O_IM2 = G::O_IM2, RS = 16 * IM_ROWB, DU = 4 * IM_ROWB;  // K-step 1 rows; tr_pair stride
+    // d3 = dH3 masked by h3 > 0 (on the chain); its K-step 0 split here, K-step 1 in block A
+    float d3[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) d3[r] = (h3[r] > 0.0f) ? w4v[r] * dy0 : 0.0f;
+    F3 d3f0, d3f1;
+    float rs[8];  // the level-1 residuals of the split in progress
+#pragma unroll
+    for (int q = 0; q < 4; q++) split_l1(d3, q, d3f0, rs);
+#pragma unroll
+    for (int q = 0; q < 4; q++) split_l2(q, d3f0, rs);
+    MHPPO_MARK(5);
+    f32x16 d2a = zero16(), d2b = zero16(), d1 = zero16();
+    F3 ad0, ad1, ha0, ha1, hb0, hb1;
+    // ---- block A: dH2^T = W3^T dH3^T, K-step 0 of both output tiles first (d3f1 is split meanwhile)
+    {
+      const F3 w00 = bw3(0, 0), w10 = bw3(1, 0), w01 = bw3(0, 1), w11 = bw3(1, 1);
+      using PL = Plan<0, 8, 8, 8, 24, 25>;
+      weave<24, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) d2a = mfma_b(w00.p[P6A[P]], d3f0.p[P6B[P]], d2a);
+            if constexpr (T == 1) d2b = mfma_b(w10.p[P6A[P]], d3f0.p[P6B[P]], d2b);
+            if constexpr (T == 2) d2a = mfma_b(w01.p[P6A[P]], d3f1.p[P6B[P]], d2a);
+            if constexpr (T == 3) d2b = mfma_b(w11.p[P6A[P]], d3f1.p[P6B[P]], d2b);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            if constexpr (U < 8) {  // d3's K-step 1 split
+              if constexpr (U % 2 == 0) split_l1(d3 + 8, U / 2, d3f1, rs);
+              else split_l2(U / 2, d3f1, rs);
+            } else if constexpr (U < 11) {  // the d3 image (slot 1)
+              img_write_pt(imw, d3f0, d3f1, U - 8);
+              lds_order();
+            } else if constexpr (U < 14) {  // the h2a image (slot 2)
+              img_write_pt(imw + O_IM2, h2as[0], h2as[1], U - 11);
+              lds_order();
+            } else if constexpr (U < 17) {
+              tr_pt(imr, DU, U - 14, ad0);
+            } else if constexpr (U < 20) {
+              tr_pt(imr + RS, DU, U - 17, ad1);
+            } else if constexpr (U < 23) {
+              tr_pt(imr + O_IM2, DU, U - 20, ha0);
+            } else if constexpr (U < 26) {
+              tr_pt(imr + O_IM2 + RS, DU, U - 23, ha1);
+              lds_order();
+            } else if constexpr (U < 29) {  // h2b's image over d3's (slot 1): the d3 reads are issued
+              img_write_pt(imw, h2bs[0], h2bs[1], U - 26);
+              lds_order();
+            } else {  // dW4: sum over rows of dy h3, per lane and register
+#pragma unroll
+              for (int r = 4 * (U - 29); r < 4 * (U - 28); r++) gW4r[r] = fmaf(dy0, h3[r], gW4r[r]);
+            }
+          });
+    }
+    MHPPO_MARK(6);
+    // ---- block B: dW3 = sum over rows of d3 (x) h2 (A = the d3 image, B = the h2a / h2b images), dB3
+    F3 f0, f1;  // d2a's split (block C's first operands)
+    {
+      using PL = Plan<0, 6, 6, 6, 30, 32>;
+      static_assert(PL::reg(2) < 12 && PL::reg(5) < 18, "image reads before their MFMAs");
+      weave<30, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) mac1(ad0.p[P6A[P]], ha0.p[P6B[P]], gW3a);
+            if constexpr (T == 1) mac1(ad1.p[P6A[P]], ha1.p[P6B[P]], gW3a);
+            if constexpr (T == 2) mac1(ad0.p[P6A[P]], hb0.p[P6B[P]], gW3b);
+            if constexpr (T == 3) mac1(ad1.p[P6A[P]], hb1.p[P6B[P]], gW3b);
+            if constexpr (T == 4) mac1_oh((P < 3 ? ad0 : ad1).p[2 - P % 3], oh[0], gBS);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            if constexpr (U < 3) {
+              tr_pt(imr, DU, U, hb0);
+            } else if constexpr (U < 6) {
+              tr_pt(imr + RS, DU, U - 3, hb1);
+              lds_order();
+            } else if constexpr (U < 14) {  // d2a masked by h2a > 0, two elements per unit
+              mask2(d2a, h2a, 2 * (U - 6));
+            } else if constexpr (U < 30) {  // d2a's split: K-step 0 -> f0, 1 -> f1
+              constexpr int V = U - 14, st = V / 8, q = (V % 8) / 2;
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = d2a[8 * st + e];
+              if constexpr (V % 2 == 0) split_l1(v, q, st ? f1 : f0, rs);
+              else split_l2(q, st ? f1 : f0, rs);
+            } else {  // d2b masked by h2b > 0 (block A's last MFMAs have landed by now)
+              mask2(d2b, h2b, 2 * (U - 30));
+            }
+          });
+    }
+    MHPPO_MARK(7);
+    // ---- block C: dH1^T = W2^T dH2^T (one accumulator chain over the four K-steps)
+    F3 f2, f3, bh0, bh1, da0;
+    {
+      const F3 w0 = bw2(0), w1 = bw2(1), w2 = bw2(2), w3 = bw2(3);
+      using PL = Plan<0, 11, 14, 11, 17, 11, 17, 24, 6>;
+      static_assert(PL::reg(7) < 12 && PL::reg(21) < 18, "d2b's split before its MFMAs");
+      weave<24, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) d1 = mfma_b(w0.p[P6A[P]], f0.p[P6B[P]], d1);
+            if constexpr (T == 1) d1 = mfma_b(w1.p[P6A[P]], f1.p[P6B[P]], d1);
+            if constexpr (T == 2) d1 = mfma_b(w2.p[P6A[P]], f2.p[P6B[P]], d1);
+            if constexpr (T == 3) d1 = mfma_b(w3.p[P6A[P]], f3.p[P6B[P]], d1);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            auto split_d2b = [&](int st, int V) {  // d2b's split: K-step 0 -> f2, 1 -> f3
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = d2b[8 * st + e];
+              if (V % 2 == 0) split_l1(v, V / 2, st ? f3 : f2, rs);
+              else split_l2(V / 2, st ? f3 : f2, rs);
+            };
+            if constexpr (U < 8) {
+              split_d2b(0, U);
+            } else if constexpr (U < 11) {  // the h1 image (slot 2: the h2a reads are issued)
+              img_write_pt(imw + O_IM2, h1s[0], h1s[1], U - 8);
+              lds_order();
+            } else if constexpr (U < 14) {
+              tr_pt(imr + O_IM2, DU, U - 11, bh0);
+            } else if constexpr (U < 22) {
+              split_d2b(1, U - 14);
+            } else if constexpr (U < 25) {
+              tr_pt(imr + O_IM2 + RS, DU, U - 22, bh1);
+              lds_order();
+            } else if constexpr (U < 28) {  // the d2a image (slot 1: the h2b reads are issued)
+              img_write_pt(imw, f0, f1, U - 25);
+              lds_order();
+            } else {
+              tr_pt(imr, DU, U - 28, da0);
+            }
+          });
+    }
+    MHPPO_MARK(8);
+    // ---- block D: dW2 = sum over rows of d2 (x) h1 (A = the d2a / d2b images, B = the h1 image), dB2
+    F3 a0, a1;
+    {
+      F3 da1, db0, db1, e0, e1;
+      using PL = Plan<0, 5, 6, 5, 11, 6, 11, 35, 33>;
+      static_assert(PL::reg(2) < 6 && PL::reg(8) < 12 && PL::reg(11) < 18, "image reads before their MFMAs");
+      weave<36, PL>(
+          [&](auto kc) {
+            constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
+            if constexpr (T == 0) mac1(da0.p[P6A[P]], bh0.p[P6B[P]], gW2a);
+            if constexpr (T == 1) mac1(da1.p[P6A[P]], bh1.p[P6B[P]], gW2a);
+            if constexpr (T == 2) mac1(db0.p[P6A[P]], bh0.p[P6B[P]], gW2b);
+            if constexpr (T == 3) mac1(db1.p[P6A[P]], bh1.p[P6B[P]], gW2b);
+            if constexpr (T == 4) mac1_oh((P < 3 ? da0 : da1).p[2 - P % 3], oh[1], gBS);
+            if constexpr (T == 5) mac1_oh((P < 3 ? db0 : db1).p[2 - P % 3], oh[2], gBS);
+          },
+          [&](auto uc) {
+            constexpr int U = decltype(uc)::value;
+            if constexpr (U < 3) {
+              tr_pt(imr + RS, DU, U, da1);
+              lds_order();
+            } else if constexpr (U < 6) {  // the d2b image (slot 2: the h1 reads are issued)
+              img_write_pt(imw + O_IM2, f2, f3, U - 3);
+              lds_order();
+            } else if constexpr (U < 9) {
+              tr_pt(imr + O_IM2, DU, U - 6, db0);
+            } else if constexpr (U < 12) {
+              tr_pt(imr + O_IM2 + RS, DU, U - 9, db1);
+            } else if constexpr (U < 20) {  // d1 masked by h1 > 0
+              mask2(d1, h1, 2 * (U - 12));
+            } else if constexpr (U < 36) {  // d1's split -> e0, e1
+              constexpr int V = U - 20, st = V / 8, q = (V % 8) / 2;
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; e++) v[e] = d1[8 * st + e];
+              if constexpr (V % 2 == 0) split_l1(v, q, st ? e1 : e0, rs);
+              else split_l2(q, st ? e1 : e0, rs);
+            } else if constexpr (U < 39) {  // the d1 image (slot 1: the d2a reads are issued)
+              img_write_pt(imw, e0, e1, U - 36);
+              lds_order();
+            } else if constexpr (U < 42) {  // dW1's A operands: 16x16x32 transposed reads
+              tr_pt(imr16, DU, U - 39, a0);
+            } else {
+              tr_pt(imr16 + 32, DU, U - 42, a1);
+            }
+          });
+    }
+    MHPPO_MARK(9);
+    // ---- block E: dW1 = sum over rows of d1 (x) [X | 1] (column 13: dB1), two 16x16x32 tiles
+    weave<12, Plan<>>(
+        [&](auto kc) {
+          constexpr int K = decltype(kc)::value, P = K % 6;
+          if constexpr (K < 6) mac1_16(a0.p[P6A[P]], xb.p[P6B[P]], gW1t[0][0]);
+          else mac1_16(a1.p[P6A[P]], xb.p[P6B[P]], gW1t[0][1]);
+        },
+        [&](auto) {});
+    lds_order();
+    MHPPO_MARK(10);
   }
 
   // this wave's partial gradient (packed torch layout) and float64 sums
@@ -1785,7 +2241,9 @@ constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3
 #ifndef MHPPO_X3_CRIT
 // the 13-input critic pass: bits 0-1 = forward fragments held in registers (1 W2, 2 W3), bit 2 =
 // dW4 in registers, bit 3 = DH2F + XCE ordering (A/B builds override)
-#define MHPPO_X3_CRIT 13  // W2's forward fragments held, dW4 in registers, DH2F + XCE (ab_crit.txt)
+// 12: dW4 in registers, DH2F + XCE, no forward fragments held (the hand-placed passes need those
+// registers; the phase-by-phase pass's best was 13: W2's forward fragments held, ab_crit.txt)
+#define MHPPO_X3_CRIT 12
 #endif
 constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
 constexpr int X3_CRIT_HB = 3 & ~((MHPPO_X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
@@ -1793,7 +2251,9 @@ constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 #ifndef MHPPO_X3_ACT
 // the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
 // fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE (A/B overrides)
-#define MHPPO_X3_ACT 62  // W3's forward fragments held too (ab_act.txt: W2's -2.8 %, ab_act2.txt: W3's -1 % more)
+// 60: both backward fragments held, dW4 in registers, DH2F + XCE, no forward fragments (the hand-placed
+// passes spill with them; the phase-by-phase pass's best was 62: W3's held, ab_act.txt / ab_act2.txt)
+#define MHPPO_X3_ACT 60
 #endif
 constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
 constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
@@ -1804,6 +2264,10 @@ constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
 #define MHPPO_X3_CA 0  // the choice actor: bits 0-1 forward fragments held, bit 3 DH2F + XCE
 #endif
 constexpr int X3_CC_HF = MHPPO_X3_CC & 3, X3_CA_HF = MHPPO_X3_CA & 3;
+#ifndef MHPPO_X3_SCH
+#define MHPPO_X3_SCH 1  // the 13-input single-net passes with the hand-placed backward (A/B builds override)
+#endif
+constexpr bool X3_SCH = MHPPO_X3_SCH;
 constexpr bool X3_CC_W4R = MHPPO_X3_CC & 4, X3_CC_ORD = MHPPO_X3_CC & 8, X3_CA_ORD = MHPPO_X3_CA & 8;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
@@ -1831,7 +2295,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   Pass<KIND, C13 ? X3_CRIT_HF : (A13 ? X3_ACT_HF : (CC ? X3_CC_HF : X3_CA_HF)),
        A13 ? X3_ACT_HB : (C13 ? X3_CRIT_HB : 3), G,
        (KIND == K_CRITIC ? X3_BS_CRITIC : X3_BS_ACTOR), ORD, ORD,
-       (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R) || (CC && X3_CC_W4R)>
+       (A13 && X3_ACT_W4R) || (C13 && X3_CRIT_W4R) || (CC && X3_CC_W4R), (A13 || C13) && X3_SCH>
       p;
   p.init(L8, ws, nin, counts, m_global);
   float meanf = 0.f, stdf = 1.f;
@@ -1873,7 +2337,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   stage_net<G>(Wc, L8 + G::NET_B, tid, NIN_CONT);
   __syncthreads();
   Pass<K_CONT, false, 0, G, X3_BS_PAIR, true> pa;  // two nets in one wave: no fragments held
-  Pass<K_CRITIC, false, 0, G, X3_BS_PAIR, true> pc;
+  Pass<K_CRITIC, false, 0, G, X3_BS_PAIR, true, false, true> pc;  // dW4 in registers as the single critic pass: the same bits
   pa.init(L8, ws);
   pc.init(L8 + G::NET_B, ws);
   float meanf, stdf;

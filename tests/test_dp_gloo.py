@@ -268,9 +268,9 @@ class _Cfg:
 class _VenvDouble:
     """The attributes Algo_PPO reads from a VecCrosswalk (CPU; no env handle)."""
 
-    def __init__(self, n_envs, env_id_offset):
+    def __init__(self, n_envs, env_id_offset, n_slots=2, variant="coop"):
         self.n_envs, self.env_id_offset = n_envs, env_id_offset
-        self.max_episode, self.n_slots, self.dt, self.variant = 8, 2, 0.5, "coop"
+        self.max_episode, self.n_slots, self.dt, self.variant = 8, n_slots, 0.5, variant
         self.cfg, self.device = _Cfg(), torch.device("cpu")
 
 
@@ -323,7 +323,7 @@ def _rollout_double_class(n_total):
     return RolloutDouble
 
 
-def _run_algo(rank, world, port, n_total, out_q):
+def _run_algo(rank, world, port, n_total, out_q, n_slots=2, variant="coop"):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "mh-ppo_amd")]
     from mhppo import algo as algo_mod
     from mhppo import ppo
@@ -335,7 +335,8 @@ def _run_algo(rank, world, port, n_total, out_q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     n = n_total // world
     torch.manual_seed(0)
-    a = algo_mod.Algo_PPO(Model_PPO, _VenvDouble(n, rank * n), verbose=False, save_curves=False, num_states_d=20)
+    a = algo_mod.Algo_PPO(Model_PPO, _VenvDouble(n, rank * n, n_slots, variant), verbose=False, save_curves=False,
+                          num_states_d=20)
     a.train(2)
     if rank == 0:
         out_q.put([p.detach().numpy().copy() for net in a.nets() for p in net.parameters()] +
@@ -344,11 +345,11 @@ def _run_algo(rank, world, port, n_total, out_q):
         dist.destroy_process_group()
 
 
-def _spawn_algo(world, n_total):
+def _spawn_algo(world, n_total, n_slots=2, variant="coop"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 31700 + os.getpid() % 1000 + world
-    procs = [ctx.Process(target=_run_algo, args=(r, world, port, n_total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run_algo, args=(r, world, port, n_total, q, n_slots, variant)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -370,3 +371,18 @@ def test_dp4_algo_train_uneven_shards():
     for a, b in zip(single, dp4):
         np.testing.assert_allclose(b, a, rtol=1e-6, atol=2e-6)
     assert len(single[-4]) == 2  # two reward-curve entries per head
+
+
+def test_dp8_algo_train_cfg5_partition():
+    """Config 5's partition (BASELINE configs[4]: the scalable env's envs split contiguously over 8
+    ranks, rank r owning global env ids [r n, (r + 1) n)) at small N: two whole Algo_PPO.train
+    iterations over 8 gloo ranks with 8 car slots per env equal one process on all envs (ranks 2-3
+    hold no wait rows, ranks 4-5 no cross rows).  The HIP path's global-id seeding for that partition
+    is pinned on one GPU at full size (tests/test_env_fullscale_gpu.py / test_rollout_fullscale_gpu.py,
+    cfg5_shard7)."""
+    n_total = 64
+    single = _spawn_algo(1, n_total, n_slots=8, variant="scalable")
+    dp8 = _spawn_algo(8, n_total, n_slots=8, variant="scalable")
+    assert len(single) == len(dp8)
+    for a, b in zip(single, dp8):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=2e-6)

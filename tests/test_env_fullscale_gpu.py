@@ -37,16 +37,21 @@ def _report(name, rec):
     print(name, json.dumps(rec))
 
 
-@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("scalable", 8, 1, 4), ("coop", 2, 1, 2)],
-                         ids=["cfg3_4cars", "cfg4_scalable", "cfg2_coop"])
+# cfg5_shard7: config 5 (524 288 scalable envs over 8 GPUs) is env-id sharded; its last rank runs
+# global ids 458 752 .. 524 287 (env_id_offset = 7 x 65 536) and must draw exactly the streams the
+# reference's env would at those ids (random.seed(seed_base + global id)) — the one config-5
+# property a single GPU can pin.
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2, 0), ("scalable", 8, 1, 4, 0), ("coop", 2, 1, 2, 0),
+                                  ("scalable", 8, 1, 4, 7 * 65536)],
+                         ids=["cfg3_4cars", "cfg4_scalable", "cfg2_coop", "cfg5_shard7_scalable"])
 def test_fullscale_discrete_parity(case):
     from mhppo.env import VecCrosswalk
     from oracle import OracleBatch, set_threads
     set_threads(min(16, os.cpu_count() or 1))
-    v, nc, npd, nl = case
+    v, nc, npd, nl, off = case
     N, T, seed = 65536, 80, 31000
-    env = VecCrosswalk(v, N, nc, npd, nl, seed_base=seed)
-    orc = OracleBatch(v, N, nc, npd, nl, seed_base=seed)
+    env = VecCrosswalk(v, N, nc, npd, nl, seed_base=seed, env_id_offset=off)
+    orc = OracleBatch(v, N, nc, npd, nl, seed_base=seed + off)  # the oracle's env e = global id off + e
     assert np.array_equal(env.reset().cpu().numpy(), orc.reset())
     k = orc.dump_dim
     S = env.n_slots
@@ -92,7 +97,7 @@ def test_fullscale_discrete_parity(case):
     mt_g, _ = env.get_rng()
     mt_o, _ = orc.rng_state()
     mt_bad = (mt_g.cpu().numpy().view(np.uint32) != mt_o).any(1)
-    rec = dict(config=f"{v} {nc}/{npd}/{nl}", envs=N, steps=T, diverged_envs=int(div.sum()),
+    rec = dict(config=f"{v} {nc}/{npd}/{nl}", envs=N, env_id_offset=off, steps=T, diverged_envs=int(div.sum()),
                mt_state_mismatch_envs=int(mt_bad.sum()), first_divergence_steps=sorted(set(first_div[div].tolist()))[:20],
                diverged_env_ids=np.nonzero(div)[0][:20].tolist(), float_outputs_bit_different=n_bits,
                float_outputs=n_tot, bit_different_fraction=n_bits / max(n_tot, 1),
@@ -100,6 +105,6 @@ def test_fullscale_discrete_parity(case):
                event_counts_gpu=dict(zip(("accident", "possible_accident", "small_mistake", "not_waiting",
                                           "bad_green"), ev_g.sum(0).tolist())),
                max_rel_err_f64_undiverged=max_rel, max_rel_err_obs_f32_undiverged=max_rel_obs)
-    _report(v, rec)
+    _report(v + (f"_offset{off}" if off else ""), rec)
     assert rec["diverged_envs"] == 0 and rec["mt_state_mismatch_envs"] == 0, rec
     assert max_rel <= 1e-9 and max_rel_obs <= 1e-6, rec

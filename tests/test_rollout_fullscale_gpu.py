@@ -45,16 +45,19 @@ def _bitdiff(a, b):
     return int((a != b).sum().item())
 
 
-@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("scalable", 8, 1, 4)], ids=["cfg3_4cars", "cfg4_scalable"])
+# cfg5_shard7: config 5's last rank (global env ids 458 752 .. 524 287, env_id_offset 7 x 65 536):
+# env streams and Philox policy noise keyed by global id (tests/test_env_fullscale_gpu.py)
+@pytest.mark.parametrize("case", [("4cars", 4, 1, 2, 0), ("scalable", 8, 1, 4, 0), ("scalable", 8, 1, 4, 7 * 65536)],
+                         ids=["cfg3_4cars", "cfg4_scalable", "cfg5_shard7_scalable"])
 def test_policy_rollout_fullscale_parity(case):
     from mhppo.env import VecCrosswalk
     from mhppo.models import Model_PPO
     from mhppo.rollout import RolloutGPU
     from oracle import OracleBatch, set_threads
     set_threads(min(16, os.cpu_count() or 1))
-    v, nc, npd, nl = case
+    v, nc, npd, nl, off = case
     N, T, seed = int(os.environ.get("MHPPO_FULLSCALE_ENVS", "65536")), 80, 41000
-    venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=seed)
+    venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=seed, env_id_offset=off)
     ro = RolloutGPU(venv)
     torch.manual_seed(5)
     ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
@@ -63,7 +66,7 @@ def test_policy_rollout_fullscale_parity(case):
     b = ro.collect(ac, aw, ad, seed=3, iteration=0)
     torch.cuda.synchronize()
     S, P = ro.S, ro.P
-    orc = OracleBatch(v, N, nc, npd, nl, seed_base=seed)
+    orc = OracleBatch(v, N, nc, npd, nl, seed_base=seed + off)  # oracle env e = global id off + e
     o = orc.rollout(ac.packed().cpu().numpy(), aw.packed().cpu().numpy(), ad.packed().cpu().numpy(),
                     u=ro.u.cpu().numpy(), eps=ro.eps.cpu().numpy(), T=T)
     dev = venv.device
@@ -119,7 +122,8 @@ def test_policy_rollout_fullscale_parity(case):
                                           "bad_green"), ev_g.sum(0).tolist())),
                diverged_env_ids=torch.nonzero(div).flatten()[:20].tolist(),
                first_reward_jump_steps=first_t[div][:20].tolist(), continuous_undiverged=cont)
-    _report(v, rec)
+    rec["env_id_offset"] = off
+    _report(v + (f"_offset{off}" if off else ""), rec)
     assert rec["diverged_envs"] == 0, rec
     for name, c in cont.items():
         assert c["max_rel_err"] <= c["tol"], (name, c)

@@ -106,6 +106,40 @@ def check_function(name, lines):
             if used & pending:
                 bad.append(f"{name}: '{ln2.strip()}' touches in-flight {pi[1][0]} of '{ln.strip()}'")
                 break
+    # The hand-placed backward's one-MFMA asm statements (mac1 / mac1_16: AGPR accumulator, no
+    # s_nop inside) rely on their A / B operands never being written by a VALU instruction in the
+    # two wait states before them (VALU write -> MFMA SrcA/B read: 2 wait states on gfx950; hipcc
+    # pads nothing around an asm statement).  Every AGPR-accumulating MFMA is checked: walking back
+    # over the instructions before it, counting one wait state per instruction and N + 1 per
+    # s_nop N, no v_* instruction within 2 wait states may write a VGPR / AGPR it reads as A or B.
+    def dst_regs(ops_):
+        t = ops_[0] if ops_ else ""
+        m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", t)
+        if m:
+            return {(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)}
+        m = re.fullmatch(r"([va])(\d+)", t)
+        return {(m.group(1), int(m.group(2)))} if m else set()
+    for n, (i, p) in enumerate(ops):
+        if not agpr_mfma(p):
+            continue
+        srcs = set()
+        for tok in p[1][1:3]:
+            m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", tok)
+            if m:
+                srcs |= {(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)}
+        states, k = 0, n - 1
+        while k >= 0 and states < 2:
+            j, q = ops[k]
+            if any(insts[x][0].strip().endswith(":") for x in range(j + 1, i)):
+                break  # a label in between: another block's tail, not this straight-line run
+            if q[0] == "s_nop":
+                states += int(q[1][0], 0) + 1
+            else:
+                if q[0].startswith("v_") and not q[0].startswith("v_mfma") and dst_regs(q[1]) & srcs:
+                    bad.append(f"{name}: '{insts[j][0].strip()}' writes an operand of '{insts[i][0].strip()}' "
+                               f"{states} wait states before it")
+                states += 1
+            k -= 1
     return bad, n_reads
 
 
