@@ -1136,7 +1136,10 @@ __device__ __forceinline__ void mac1_16(const u32x4 &a, const u32x4 &b, f32x4 &c
 // where the source puts it, and the machine scheduler never moves an instruction across a region
 // barrier.  (Pinning the units with empty volatile asm statements instead cost one copy and one
 // wait state per pinned value.)
-__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+// opaque loaded values: unconditional loads (hipcc otherwise turns `cond ? load : const` into a
+// branch around the load); all of a unit's loads are pinned in ONE statement, after the last one
+// is issued, so they wait once, together
+__device__ __forceinline__ void pin4(float *v) { asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])); }
 // split level 1 of element pair q of an 8-element fragment v: hi part, residuals r[2q], r[2q+1]
 __device__ __forceinline__ void split_l1(const float *v, int q, F3 &f, float *r) {
   const uint32_t h = pk_bf16(v[2 * q], v[2 * q + 1]);
@@ -1278,6 +1281,9 @@ struct Pass {
   const double *counts;  // K_CHOICE: the global action counts (nullptr: per-row mode)
   double m_global;
   F3 wf2[2][2], wf3[4], wb3[2][2], wb2[4];
+  // SCH: the previous tile's dW1 block (E), deferred into this tile's layer-1 shadows: its A operands
+  // (the d1 image's transposed reads) and B operand (the input columns); zero before the first tile
+  F3 ea0, ea1, exb;
   f32x16 gW2a, gW2b, gW3a, gW3b;
   f32x4 gW1t[KS1][2];
   f32x16 gBS;    // BS: column 0 = dB3, 1 = dB2[0:32], 2 = dB2[32:64] (rows = out features)
@@ -1334,9 +1340,15 @@ struct Pass {
     }
     if constexpr (BS) {
       gBS = zero16();
+      if constexpr (SCH) {
+        for (int q = 0; q < 3; q++) ea0.p[q] = ea1.p[q] = exb.p[q] = u32x4{0u, 0u, 0u, 0u};
+      }
       for (int q = 0; q < 3; q++) {
         const uint32_t v = j == q ? 0x3f803f80u : 0u;
         oh[q] = u32x4{v, v, v, v};
+        // opaque (not a rematerialisable constant): the compiler would rebuild it with a
+        // v_accvgpr_write right before its MFMA, a write the MFMA reads without wait states
+        if constexpr (SCH) asm volatile("" : "+a"(oh[q]));
       }
     }
   }
@@ -1390,7 +1402,9 @@ struct Pass {
       relu16(h);
       return h;
     };
-    f32x16 h1 = layer1();
+    f32x16 h1;
+    if constexpr (SCH) h1 = layer1_s(ws, Xs);
+    else h1 = layer1();
     x3_phase();
     MHPPO_MARK(2);
     // ---- layer 2 (the biases ride in as the chains' initial accumulators)
@@ -1694,6 +1708,62 @@ struct Pass {
     MHPPO_MARK(9);
   }
 
+  // The previous tile's dW1 block E: 12 AGPR MFMAs (16x16x32) on the deferred operands
+  template <int K>
+  __device__ __forceinline__ void mac_e() {
+    constexpr int P = K % 6;
+    if constexpr (K < 6) mac1_16(ea0.p[P6A[P]], exb.p[P6B[P]], gW1t[0][0]);
+    else mac1_16(ea1.p[P6A[P]], exb.p[P6B[P]], gW1t[0][1]);
+  }
+  // Layer 1 of one tile, hand-placed (SCH), with the PREVIOUS tile's dW1 block in its shadows: the
+  // input loads first, then E's MFMAs carry the input split, then layer 1's six MFMAs alternate with
+  // E's last ones.  (E used to end the tile: twelve 16-cycle MFMAs with nothing beside them, behind
+  // the LDS latency of their operand reads; deferred, its operands are already in registers.)  The
+  // per-accumulator product order is unchanged: the same bits.  Returns ReLU(h1).
+  __device__ __forceinline__ f32x16 layer1_s(const WaveSlot<G> &ws, const float *Xs) {
+    const int j = ws.j, kh = ws.kh;
+    float v8[8], rs[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) v8[q] = Xs[j * NIN_CONT + 8 * kh + q];  // past column 12: unused
+    pin4(v8);
+    pin4(v8 + 4);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {  // row j, input column 8h + q (the bias input at column 13)
+      const int k = 8 * kh + q;
+      v8[q] = k < NIN_CONT ? v8[q] : (k == NIN_CONT ? 1.0f : 0.0f);
+    }
+    const F3 w1 = rd_pair<G::W1_PART>(w1row, 8);
+    F3 xs;
+    f32x16 h = zero16();
+    // regions: E0 E1 | E2..E9 + the input split | L0 E10 L1 E11 L2 L3 L4 L5
+    constexpr int ORD[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 100, 10, 101, 11, 102, 103, 104, 105};
+    weave<18, Plan<2, 10, 8>>(
+        [&](auto kc) {
+          constexpr int K = decltype(kc)::value, M = ORD[K];
+          if constexpr (M < 100) mac_e<M>();
+          else h = mfma_b(w1.p[P6A[M - 100]], xs.p[P6B[M - 100]], h);
+        },
+        [&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          if constexpr (U % 2 == 0) split_l1(v8, U / 2, xs, rs);
+          else split_l2(U / 2, xs, rs);
+        });
+    relu16(h);
+    return h;
+  }
+  // after the tile loop: the last tile's deferred dW1 block (once per launch: every MFMA behind
+  // enough wait states for a compiler copy of its accumulator or operands just before it)
+  __device__ __forceinline__ void drain() {
+    if constexpr (SCH) {
+      sfor<0, 12>([&](auto kc) {
+        constexpr int K = decltype(kc)::value, P = K % 6;
+        f32x4 &c = K < 6 ? gW1t[0][0] : gW1t[0][1];
+        const F3 &a = K < 6 ? ea0 : ea1;
+        asm volatile("s_nop 4\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a.p[P6A[P]]), "v"(exb.p[P6B[P]]));
+      });
+    }
+  }
+
   // Layers 2 and 3 of one tile, hand-placed (SCH): each layer's MFMAs carry the splits its own later
   // K-steps and the next layer need (the same products in the same order per accumulator as the
   // plain forward, so the same bits):
@@ -1735,12 +1805,12 @@ struct Pass {
               else split_l2(U / 2, h1s[1], rs);
             } else if constexpr (U < 10) {  // dW1's B operand: rows 8G .. 8G + 7 of input column l & 15
               const int n = l & 15, nc = n < NIN_CONT ? n : NIN_CONT - 1;
+              float v[4];
 #pragma unroll
-              for (int q = 4 * (U - 8); q < 4 * (U - 7); q++) {
-                float v = Xs[(8 * G_ + q) * NIN_CONT + nc];
-                pin(v);  // an unconditional load (a select, not a branch around it)
-                xv[q] = n < NIN_CONT ? v : (n == NIN_CONT ? 1.0f : 0.0f);
-              }
+              for (int q = 0; q < 4; q++) v[q] = Xs[(8 * G_ + 4 * (U - 8) + q) * NIN_CONT + nc];
+              pin4(v);
+#pragma unroll
+              for (int q = 0; q < 4; q++) xv[4 * (U - 8) + q] = n < NIN_CONT ? v[q] : (n == NIN_CONT ? 1.0f : 0.0f);
             } else if constexpr (U < 18) {
               constexpr int V = U - 10;
               if constexpr (V % 2 == 0) split_l1(xv, V / 2, xb, rt);
@@ -2008,16 +2078,12 @@ struct Pass {
           });
     }
     MHPPO_MARK(9);
-    // ---- block E: dW1 = sum over rows of d1 (x) [X | 1] (column 13: dB1), two 16x16x32 tiles
-    weave<12, Plan<>>(
-        [&](auto kc) {
-          constexpr int K = decltype(kc)::value, P = K % 6;
-          if constexpr (K < 6) mac1_16(a0.p[P6A[P]], xb.p[P6B[P]], gW1t[0][0]);
-          else mac1_16(a1.p[P6A[P]], xb.p[P6B[P]], gW1t[0][1]);
-        },
-        [&](auto) {});
+    // ---- block E: dW1 = sum over rows of d1 (x) [X | 1] (column 13: dB1), two 16x16x32 tiles,
+    // deferred into the next tile's layer-1 shadows (layer1_s; the last tile's: drain)
+    ea0 = a0;
+    ea1 = a1;
+    exb = xb;
     lds_order();
-    MHPPO_MARK(10);
   }
 
   // this wave's partial gradient (packed torch layout) and float64 sums
@@ -2307,6 +2373,7 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
         p.tile(ws, slot, row0, nrows, V, meanf, stdf, inv_m, out_mean, out_std);
       },
       true);
+  p.drain();
   const int np = Packed(geo_nin<G>(nin), G::NOUT).NP;
   fold_partials<G>(p, ws, L8, w, tid, np, gpart + (size_t)blockIdx.x * np, dpart + blockIdx.x * 3);
 }

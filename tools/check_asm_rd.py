@@ -108,10 +108,11 @@ def check_function(name, lines):
                 break
     # The hand-placed backward's one-MFMA asm statements (mac1 / mac1_16: AGPR accumulator, no
     # s_nop inside) rely on their A / B operands never being written by a VALU instruction in the
-    # two wait states before them (VALU write -> MFMA SrcA/B read: 2 wait states on gfx950; hipcc
+    # two wait states before them (VALU write -> MFMA SrcA/B/C read: 2 wait states on gfx950; hipcc
     # pads nothing around an asm statement).  Every AGPR-accumulating MFMA is checked: walking back
     # over the instructions before it, counting one wait state per instruction and N + 1 per
-    # s_nop N, no v_* instruction within 2 wait states may write a VGPR / AGPR it reads as A or B.
+    # s_nop N, no v_* instruction within 2 wait states may write a VGPR / AGPR it reads as A, B or C
+    # (a v_accvgpr_mov / _write of an accumulator the compiler moved between registers).
     def dst_regs(ops_):
         t = ops_[0] if ops_ else ""
         m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", t)
@@ -123,7 +124,7 @@ def check_function(name, lines):
         if not agpr_mfma(p):
             continue
         srcs = set()
-        for tok in p[1][1:3]:
+        for tok in p[1][1:4]:  # A, B and C (an accumulator a compiler copy / write just set up)
             m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", tok)
             if m:
                 srcs |= {(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)}

@@ -17,7 +17,7 @@ from mhppo.models import Model_PPO  # noqa: E402
 # MHPPO_X3_SCH=0 builds: the phase-by-phase marks
 PH_SCH = {1: "tile inputs wait", 2: "layer 1 (+h1 s0 split)", 3: "layer 2 (+payload)", 4: "layer 3 (+payload)",
           5: "loss + d3 + d3 s0 split", 6: "A dH2 (+payload)", 7: "B dW3 (+payload)", 8: "C dH1 (+payload)",
-          9: "D dW2 (+payload)", 10: "E dW1"}
+          9: "D dW2 (+payload)"}  # E (dW1) runs in the next tile's layer 1
 PH_OLD = {1: "tile inputs wait", 2: "layer 1", 3: "layer 2", 4: "layer 3", 5: "loss + dW4/dB3 sums",
           6: "dW3", 7: "dH2 + masks + dB2 sums", 8: "dW2 + dH1", 9: "dW1"}
 PH = PH_OLD if os.environ.get("X3_PHASES_OLD") else PH_SCH
