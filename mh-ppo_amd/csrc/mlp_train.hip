@@ -187,6 +187,13 @@ __device__ __forceinline__ void bias_relu(f32x16 &v, const float *b, int kh) {
 }
 // the C-layout broadcast of a per-feature vector b (register r of lane half kh = b[feature]):
 // a bias as an MFMA chain's initial accumulator, or w4 for the output layer
+// x[l] + x[l ^ 32] (the two half-wave partial sums of a row) through v_permlane32_swap: no LDS
+// round trip on the loss section's serial chain (ds_bpermute's latency).  The same bits as
+// x + __shfl_xor(x, 32): lanes 32-63 add the same two values in the other order.
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 __device__ __forceinline__ f32x16 feat_vec(const float *b, int kh) {
   const float4 *b4 = reinterpret_cast<const float4 *>(b);
   f32x16 v;
@@ -238,10 +245,18 @@ __device__ __forceinline__ float row_sum(const float *T, int l) {
 // Inputs of one full 32-row tile -> an input slot, by LDS-DMA (no VGPRs, no wait here).
 // X: 416 contiguous floats = 104 16-B chunks (64 + 40 lanes); s0/s1: one dword per lane,
 // exec masks pick the lanes (a DMA's inactive lanes write nothing).
+// Every DMA's buffer range is bounded by the rows the batch really has past row0 (M): a tile index
+// past the batch (a prefetch-ring or tile-loop indexing error) reads zeros instead of touching
+// memory outside the buffers (the raw-buffer range check bounds the offset from the base; with a
+// zero range nothing is fetched, whatever the base).  Full tiles: the same 32-row ranges.
+__device__ __forceinline__ uint32_t tile_rows(int64_t M, int64_t row0) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)max((int64_t)0, min((int64_t)32, M - row0)));
+}
 template <int KIND, class LY>
 __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const float *ret, const float *V,
-                                              const float *act, const float *lp, int64_t row0, int l) {
-  const v4i rx = rsrc_v(X + row0 * NIN_CONT, 32 * NIN_CONT * 4);
+                                              const float *act, const float *lp, int64_t row0, int l, int64_t M) {
+  const uint32_t rows = tile_rows(M, row0);
+  const v4i rx = rsrc_v(X + row0 * NIN_CONT, rows * NIN_CONT * 4);
   // Every DMA on all 64 lanes (no exec-mask branches): an LDS-DMA lane writes base + 4 lane, so
   // the lanes past a piece's end land in the NEXT piece's place (or the 32-float pad after s1),
   // reading zeros past their buffer's bounds; the pieces are issued in address order and their
@@ -249,11 +264,11 @@ __device__ __forceinline__ void prefetch_tile(float *slot, const float *X, const
   dma16(rx, slot + LY::IN_X, 16 * l);
   dma16(rx, slot + LY::IN_X + 256, 1024 + 16 * l);  // X 256..415; lanes 40-63: zeros into s0
   const uint32_t vo = 4 * l;
-  dma4(rsrc_v(ret + row0, 128), slot + LY::IN_S0, vo);  // ret [0, 32); lanes 32-63: zeros [32, 64)
+  dma4(rsrc_v(ret + row0, 4 * rows), slot + LY::IN_S0, vo);  // ret [0, 32); lanes 32-63: zeros [32, 64)
   if (KIND == K_CONT) {
-    dma4(rsrc_v(V + row0, 128), slot + LY::IN_S0 + 32, vo);   // V [32, 64); overhang into s1
-    dma4(rsrc_v(act + row0, 128), slot + LY::IN_S1, vo);      // act [0, 32); overhang [32, 64)
-    dma4(rsrc_v(lp + row0, 128), slot + LY::IN_S1 + 32, vo);  // logp_old [32, 64); overhang: pad
+    dma4(rsrc_v(V + row0, 4 * rows), slot + LY::IN_S0 + 32, vo);   // V [32, 64); overhang into s1
+    dma4(rsrc_v(act + row0, 4 * rows), slot + LY::IN_S1, vo);      // act [0, 32); overhang [32, 64)
+    dma4(rsrc_v(lp + row0, 4 * rows), slot + LY::IN_S1 + 32, vo);  // logp_old [32, 64); overhang: pad
   }
 }
 template <int KIND>
@@ -396,7 +411,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 
   int cb = 0;
   MHPPO_MARK(0);
-  if (PF && gw < nfull) prefetch_tile<KIND, LY>(ws + LY::O_IN, X, ret, V, act, lp_old, gw * 32, l);
+  if (PF && gw < nfull) prefetch_tile<KIND, LY>(ws + LY::O_IN, X, ret, V, act, lp_old, gw * 32, l, M);
   TileRegs<LY> tnext;  // non-PF: the next tile's inputs in registers
   if (!PF && gw < ntiles)
     load_tile_regs<KIND, LY>(tnext, X, nin, ret, V, act, lp_old, gw * 32, (int)min((int64_t)32, M - gw * 32), l);
@@ -407,7 +422,7 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
     if constexpr (PF) {
       const int64_t nxt = tile + nw;
       if (nxt < nfull) {
-        prefetch_tile<KIND, LY>(ws + LY::O_IN + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l);
+        prefetch_tile<KIND, LY>(ws + LY::O_IN + (cb ^ 1) * LY::IN_SZ, X, ret, V, act, lp_old, nxt * 32, l, M);
         wait_vmcnt<prefetch_ops<KIND>()>();  // this tile's DMA (issued one iteration earlier) has landed
       } else if (tile < nfull) {
         wait_vmcnt<0>();
@@ -763,9 +778,9 @@ constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 // nin <= K1 - 1).  LDS: the net's weights (bf16 images of W1..W3, f32 b2 b3 w4 b4), then per
 // wave: the tile image (also the f32 transpose image), two input slots (double buffered), a
 // second tile image.
-template <int K1_, int NOUT_, int NIC_>
+template <int K1_, int NOUT_, int NIC_, int NIM_ = 2>
 struct Geo {
-  static constexpr int K1 = K1_, KS1 = K1 / 16, NOUT = NOUT_, NIC = NIC_;
+  static constexpr int K1 = K1_, KS1 = K1 / 16, NOUT = NOUT_, NIC = NIC_, NIM = NIM_;
   static_assert(K1 % 16 == 0 && (NIC == 0 || NIC < K1), "layer-1 geometry");
   static constexpr int W1_ROWB = 2 * K1 + 8, W1_PART = 32 * W1_ROWB;
   static constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_F = O_W3 + 3 * W3_PART;
@@ -776,7 +791,11 @@ struct Geo {
   static constexpr int XMAX = NIC ? (32 * NIC + 3) / 4 * 4 : (32 * (K1 - 1) + 255) / 256 * 256;
   static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = XMAX + 64, IN_SZ = XMAX + 128 + (NIC ? 32 : 0);
   static constexpr int XPIECES = (XMAX * 4 + 1023) / 1024;
-  static constexpr int O_IN = (IMG + 15) / 16 * 16, O_IM2 = O_IN + 2 * IN_SZ * 4, WAVE_B = O_IM2 + (IMG + 15) / 16 * 16;
+  // NIM tile-image slots per wave: slot 1 at 0, slot 2 at O_IM2, slots 3 and 4 after it (the
+  // hand-placed passes write the forward's h1 / h2a images during the forward, into slots of their own)
+  static constexpr int IMGA = (IMG + 15) / 16 * 16;
+  static constexpr int O_IN = IMGA, O_IM2 = O_IN + 2 * IN_SZ * 4, O_IM3 = O_IM2 + IMGA, O_IM4 = O_IM3 + IMGA,
+                       WAVE_B = O_IM2 + (NIM - 1) * IMGA;
   static constexpr int LDS_BYTES = NET_B + WAVES * WAVE_B;
   static constexpr int LDS_BYTES_PAIR = 2 * NET_B + WAVES * WAVE_B;  // two nets' weights (pair kernel)
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -784,6 +803,7 @@ struct Geo {
 };
 // the 13-input continuous heads (the big batches): the slot layout of the f32 path's Lay<7, true, 1>
 using G13 = Geo<16, 1, NIN_CONT>;
+using G13S = Geo<16, 1, NIN_CONT, 4>;  // the hand-placed single-net passes (four image slots per wave)
 using LY = Lay<7, true, 1>;
 static_assert(G13::IN_S0 == LY::IN_S0 && G13::IN_S1 == LY::IN_S1 && G13::IN_SZ == LY::IN_SZ, "13-input slot");
 static_assert(G13::LDS_BYTES_PAIR <= 160 * 1024, "LDS budget (pair)");
@@ -1001,6 +1021,15 @@ __device__ __forceinline__ void img_write_pt(char *wbase, const F3 &f0, const F3
     const int q = 2 * (g & 1);
     *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 16 * g) = make_uint2(f.p[pt][q], f.p[pt][q + 1]);
   }
+}
+// one half of img_write_pt: ONE 16-byte-per-lane LDS store (a ds_write2_b64), register groups 2 hf
+// and 2 hf + 1 of part pt (f = f0 for hf 0, f1 for hf 1).  The hand-placed passes issue an image as
+// six of these, at most one per two MFMA shadows: with four waves storing, a store after every MFMA
+// costs each wave 27 cycles per store, two after every MFMA 95, one after every second MFMA nothing
+// (tools/probes/lds_store_mfma.hip, profiles/r05_lds_store/)
+__device__ __forceinline__ void img_write_h(char *wbase, const F3 &f, int pt, int hf) {
+  *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 32 * hf) = make_uint2(f.p[pt][0], f.p[pt][1]);
+  *reinterpret_cast<uint2 *>(wbase + pt * IM_PART + 32 * hf + 16) = make_uint2(f.p[pt][2], f.p[pt][3]);
 }
 // one part of a transposed fragment read (tr_pair): two ds_read_b64_tr_b16
 __device__ __forceinline__ void tr_pt(const char *p, int du, int pt, F3 &f) {
@@ -1411,8 +1440,9 @@ struct Pass {
     f32x16 h2a = feat_vec(F, kh), h2b = feat_vec(F + 32, kh);
     f32x16 h3 = feat_vec(F + 64, kh);
     F3 h1s[2], h2as[2], h2bs[2], xb;  // SCH: the forward's splits (kept for the backward's images)
+    F3 sha0, sha1;                    // SCH: dW3's B operands (the h2a image's reads, in layer 3's shadows)
     if constexpr (SCH) {
-      fwd_s(ws, Xs, h1, h1s, h2a, h2b, h2as, h2bs, h3, xb);
+      fwd_s(ws, Xs, h1, h1s, h2a, h2b, h2as, h2bs, h3, xb, sha0, sha1);
     } else {
 #pragma unroll
       for (int s = 0; s < 2; s++) {
@@ -1438,7 +1468,7 @@ struct Pass {
     float part0 = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; r++) part0 = fmaf(w4v[r], h3[r], part0);
-    const float y0 = (part0 + __shfl_xor(part0, 32)) + b40;
+    const float y0 = xhalf_sum(part0) + b40;
     f32x16 w4v1;
     float y1 = 0.0f;
     if constexpr (NOUT == 2) {
@@ -1446,7 +1476,7 @@ struct Pass {
       float part1 = 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; r++) part1 = fmaf(w4v1[r], h3[r], part1);
-      y1 = (part1 + __shfl_xor(part1, 32)) + b41;
+      y1 = xhalf_sum(part1) + b41;
     }
     const bool valid = j < nrows;
     float dy0 = 0.0f, dy1 = 0.0f;
@@ -1517,7 +1547,7 @@ struct Pass {
     radd(4, (kh == 0) ? dy0 : 0.0f);
     if constexpr (NOUT == 2) radd(6, (kh == 0) ? dy1 : 0.0f);
     if constexpr (SCH) {
-      bwd_s(ws, h1, h1s, h2a, h2b, h2as, h2bs, h3, w4v, dy0, xb);
+      bwd_s(ws, h1, h2a, h2b, h3, w4v, dy0, xb, sha0, sha1);
       return;
     }
     // ---- layer 4 backward: d3 = dH3^T masked; dW4 = row sums of dy h3; dB3 = row sums of d3
@@ -1774,8 +1804,11 @@ struct Pass {
   // applies its ReLU) and ReLU'd for h2a / h2b.
   __device__ __forceinline__ void fwd_s(const WaveSlot<G> &ws, const float *Xs, const f32x16 &h1, F3 (&h1s)[2],
                                         f32x16 &h2a, f32x16 &h2b, F3 (&h2as)[2], F3 (&h2bs)[2], f32x16 &h3,
-                                        F3 &xb) {
+                                        F3 &xb, F3 &ha0, F3 &ha1) {
     const int l = ws.l, G_ = ws.G;
+    char *imw = ws.imw;
+    const char *imr = ws.imr;
+    constexpr int RS = 16 * IM_ROWB, DU = 4 * IM_ROWB;
     float rs[8], rt[8], xv[8];
     float h1v[16];
 #pragma unroll
@@ -1787,9 +1820,10 @@ struct Pass {
     {
       const F3 w00 = fw2(0, 0), w01 = fw2(0, 1), w10 = fw2(1, 0), w11 = fw2(1, 1);
       // h1 s1 split (8 units, before k = 6), dW1's B operand (1 + 8), h2a ReLU (4, after its last
-      // MFMA k = 11 has landed) + h2a s0 split (8) + h2a s1 split level 1 (4)
-      using PL = Plan<0, 5, 8, 5, 12, 10, 13, 24, 16>;
-      static_assert(PL::reg(7) < 6, "h1's K-step 1 before its MFMAs");
+      // MFMA k = 11 has landed) + h2a s0 split (8) + h2a s1 split level 1 (4); the h1 image (slot 3,
+      // six stores, one per two shadows; its K-step 1 half after that split)
+      using PL = Plan<0, 5, 8, 5, 12, 10, 13, 24, 16, 1, 13, 6>;
+      static_assert(PL::reg(7) < 6 && PL::reg(7) < PL::reg(37), "h1's K-step 1 before its MFMAs and its image");
       weave<24, PL>(
           [&](auto kc) {
             constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
@@ -1824,11 +1858,15 @@ struct Pass {
               for (int e = 0; e < 8; e++) v[e] = h2a[e];
               if constexpr (V % 2 == 0) split_l1(v, V / 2, h2as[0], rs);
               else split_l2(V / 2, h2as[0], rs);
-            } else {  // h2a K-step 1 split, level 1 (level 2 in L3)
+            } else if constexpr (U < 34) {  // h2a K-step 1 split, level 1 (level 2 in L3)
               float v[8];
 #pragma unroll
               for (int e = 0; e < 8; e++) v[e] = h2a[8 + e];
               split_l1(v, U - 30, h2as[1], rt);
+            } else {  // the h1 image (slot 3): part (U - 34) % 3 of K-step half (U - 34) / 3
+              constexpr int V = U - 34;
+              img_write_h(imw + G::O_IM3, h1s[V / 3], V % 3, V / 3);
+              lds_order();
             }
           });
     }
@@ -1836,9 +1874,14 @@ struct Pass {
     {
       const F3 w0 = fw3(0), w1 = fw3(1), w2 = fw3(2), w3 = fw3(3);
       // h2a s1 level 2 (4, before k = 6) + h2b ReLU 0-7 (2) + h2b s0 level 1 (4); h2b s0 level 2 (4,
-      // before k = 12) + h2b ReLU 8-15 (2) + h2b s1 level 1 (4); h2b s1 level 2 (4, before k = 18)
-      using PL = Plan<0, 6, 10, 6, 12, 10, 12, 18, 4>;
+      // before k = 12) + h2b ReLU 8-15 (2) + h2b s1 level 1 (4); h2b s1 level 2 (4, before k = 18);
+      // the h2a image (slot 4) and the h2b image (slot 2), one store per two shadows, each half after
+      // its split; the h2a image's transposed reads (dW3's B operands) behind its stores
+      using PL = Plan<0, 6, 10, 6, 12, 10, 12, 18, 4, 1, 13, 6, 13, 25, 6, 12, 24, 6>;
       static_assert(PL::reg(3) < 6 && PL::reg(13) < 12 && PL::reg(23) < 18, "splits before their MFMAs");
+      static_assert(PL::reg(3) < PL::reg(27) && PL::reg(13) < PL::reg(30) && PL::reg(23) < PL::reg(33) &&
+                        PL::reg(29) < PL::reg(36),
+                    "image halves after their splits, reads after the stores");
       weave<24, PL>(
           [&](auto kc) {
             constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
@@ -1867,34 +1910,49 @@ struct Pass {
 #pragma unroll
               for (int e = 0; e < 8; e++) v[e] = h2b[8 + e];
               split_l1(v, U - 16, h2bs[1], rt);
-            } else {
+            } else if constexpr (U < 24) {
               split_l2(U - 20, h2bs[1], rt);
+            } else if constexpr (U < 30) {  // the h2a image (slot 4)
+              constexpr int V = U - 24;
+              img_write_h(imw + G::O_IM4, h2as[V / 3], V % 3, V / 3);
+              lds_order();
+            } else if constexpr (U < 36) {  // the h2b image (slot 2: the previous tile's d2b reads are issued)
+              constexpr int V = U - 30;
+              img_write_h(imw + G::O_IM2, h2bs[V / 3], V % 3, V / 3);
+              lds_order();
+            } else if constexpr (U < 39) {
+              tr_pt(imr + G::O_IM4, DU, U - 36, ha0);
+            } else {
+              tr_pt(imr + G::O_IM4 + RS, DU, U - 39, ha1);
+              lds_order();
             }
           });
     }
   }
 
   // The backward of one tile, hand-placed (SCH): five MFMA blocks, each carrying the work the
-  // next block needs in its MFMA shadows (the plans below place it; an image's stores and reads go
-  // one part (hi / mid / lo) per unit, at most two stores or two reads in a shadow):
-  //   A  dH2 = W3^T d3      24 on-chain MFMAs | d3's K-step-1 split, the d3 / h2a / h2b images and
-  //                                             their reads, dW4 sums
+  // next block needs in its MFMA shadows (the plans below place it).  An image goes out as six
+  // single stores at most one per two shadows (img_write_h: LDS stores, not the MFMAs, otherwise set
+  // the pace), its reads one part (two ds_read_b64_tr_b16) per unit:
+  //   A  dH2 = W3^T d3      24 on-chain MFMAs | d3's K-step-1 split, the d3 image and its reads, dW4 sums
   //   B  dW3 (+ dB3)        30 AGPR MFMAs     | the h2b image reads, d2a / d2b masks, d2a's split
-  //   C  dH1 = W2^T d2      24 on-chain MFMAs | d2b's split, the h1 / d2a images and their reads
+  //   C  dH1 = W2^T d2      24 on-chain MFMAs | d2b's split, the d2a / d2b images, the h1 / d2a reads
   //   D  dW2 (+ dB2)        36 AGPR MFMAs     | the d2 image reads, d1's mask and split, d1's image
   //                                             and dW1's operand reads
-  //   E  dW1 (+ dB1)        12 AGPR MFMAs (16x16x32)
-  // The same products in the same order per accumulator as the phase-by-phase backward (the same
-  // bits); an image slot is rewritten only after its last reads were issued (a wave's LDS
-  // operations execute in order).  h1s / h2as / h2bs: the forward's splits (the image data);
-  // xb: dW1's B operand (input columns), split in the forward.
-  __device__ __forceinline__ void bwd_s(const WaveSlot<G> &ws, const f32x16 &h1, const F3 (&h1s)[2], const f32x16 &h2a,
-                                        const f32x16 &h2b, const F3 (&h2as)[2], const F3 (&h2bs)[2],
-                                        const f32x16 &h3, const f32x16 &w4v, float dy0, const F3 &xb) {
-    static_assert(KS1 == 1 && NOUT == 1 && BS && W4R && G::NIC == NIN_CONT, "SCH: the 13-input single-net passes");
+  //   E  dW1 (+ dB1)        12 AGPR MFMAs (16x16x32), deferred into the next tile's layer 1
+  // The forward wrote the h1 (slot 3), h2a (slot 4) and h2b (slot 2) images and read h2a's (ha0,
+  // ha1).  Slot 1: d3, then d2a, then d1; slot 2: h2b, then d2b.  The same products in the same order
+  // per accumulator as the phase-by-phase backward (the same bits); an image slot is rewritten only
+  // after its last reads were issued (a wave's LDS operations execute in order).  xb: dW1's B operand
+  // (input columns), split in the forward.
+  __device__ __forceinline__ void bwd_s(const WaveSlot<G> &ws, const f32x16 &h1, const f32x16 &h2a, const f32x16 &h2b,
+                                        const f32x16 &h3, const f32x16 &w4v, float dy0, const F3 &xb, const F3 &ha0,
+                                        const F3 &ha1) {
+    static_assert(KS1 == 1 && NOUT == 1 && BS && W4R && G::NIC == NIN_CONT && G::NIM == 4,
+                  "SCH: the 13-input single-net passes, four image slots");
     char *imw = ws.imw;
     const char *imr = ws.imr, *imr16 = ws.imr16;
-    constexpr int O_IM2 = G::O_IM2, RS = 16 * IM_ROWB, DU = 4 * IM_ROWB;  // K-step 1 rows; tr_pair stride
+    constexpr int O_IM2 = G::O_IM2, O_IM3 = G::O_IM3, RS = 16 * IM_ROWB, DU = 4 * IM_ROWB;  // K-step 1 rows; tr_pair stride
     // d3 = dH3 masked by h3 > 0 (on the chain); its K-step 0 split here, K-step 1 in block A
     float d3[16];
 #pragma unroll
@@ -1907,11 +1965,14 @@ struct Pass {
     for (int q = 0; q < 4; q++) split_l2(q, d3f0, rs);
     MHPPO_MARK(5);
     f32x16 d2a = zero16(), d2b = zero16(), d1 = zero16();
-    F3 ad0, ad1, ha0, ha1, hb0, hb1;
+    F3 ad0, ad1, hb0, hb1;
     // ---- block A: dH2^T = W3^T dH3^T, K-step 0 of both output tiles first (d3f1 is split meanwhile)
     {
       const F3 w00 = bw3(0, 0), w10 = bw3(1, 0), w01 = bw3(0, 1), w11 = bw3(1, 1);
-      using PL = Plan<0, 8, 8, 8, 24, 25>;
+      // d3f1 split (8), the d3 image (K-step 0 half in 1 3 5, K-step 1 half in 9 11 13), its reads
+      // (14 .. 19), dW4 (20 .. 23)
+      using PL = Plan<0, 8, 8, 1, 7, 3, 9, 15, 3, 14, 20, 6, 20, 24, 4>;
+      static_assert(PL::reg(7) < PL::reg(11) && PL::reg(13) < PL::reg(14), "split, then stores, then reads");
       weave<24, PL>(
           [&](auto kc) {
             constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
@@ -1925,27 +1986,18 @@ struct Pass {
             if constexpr (U < 8) {  // d3's K-step 1 split
               if constexpr (U % 2 == 0) split_l1(d3 + 8, U / 2, d3f1, rs);
               else split_l2(U / 2, d3f1, rs);
-            } else if constexpr (U < 11) {  // the d3 image (slot 1)
-              img_write_pt(imw, d3f0, d3f1, U - 8);
-              lds_order();
-            } else if constexpr (U < 14) {  // the h2a image (slot 2)
-              img_write_pt(imw + O_IM2, h2as[0], h2as[1], U - 11);
+            } else if constexpr (U < 14) {  // the d3 image (slot 1: the previous tile's d1 reads are issued)
+              constexpr int V = U - 8;
+              img_write_h(imw, V < 3 ? d3f0 : d3f1, V % 3, V / 3);
               lds_order();
             } else if constexpr (U < 17) {
               tr_pt(imr, DU, U - 14, ad0);
             } else if constexpr (U < 20) {
               tr_pt(imr + RS, DU, U - 17, ad1);
-            } else if constexpr (U < 23) {
-              tr_pt(imr + O_IM2, DU, U - 20, ha0);
-            } else if constexpr (U < 26) {
-              tr_pt(imr + O_IM2 + RS, DU, U - 23, ha1);
-              lds_order();
-            } else if constexpr (U < 29) {  // h2b's image over d3's (slot 1): the d3 reads are issued
-              img_write_pt(imw, h2bs[0], h2bs[1], U - 26);
               lds_order();
             } else {  // dW4: sum over rows of dy h3, per lane and register
 #pragma unroll
-              for (int r = 4 * (U - 29); r < 4 * (U - 28); r++) gW4r[r] = fmaf(dy0, h3[r], gW4r[r]);
+              for (int r = 4 * (U - 20); r < 4 * (U - 19); r++) gW4r[r] = fmaf(dy0, h3[r], gW4r[r]);
             }
           });
     }
@@ -1966,10 +2018,10 @@ struct Pass {
           },
           [&](auto uc) {
             constexpr int U = decltype(uc)::value;
-            if constexpr (U < 3) {
-              tr_pt(imr, DU, U, hb0);
+            if constexpr (U < 3) {  // the h2b image (slot 2, written in layer 3)
+              tr_pt(imr + O_IM2, DU, U, hb0);
             } else if constexpr (U < 6) {
-              tr_pt(imr + RS, DU, U - 3, hb1);
+              tr_pt(imr + O_IM2 + RS, DU, U - 3, hb1);
               lds_order();
             } else if constexpr (U < 14) {  // d2a masked by h2a > 0, two elements per unit
               mask2(d2a, h2a, 2 * (U - 6));
@@ -1990,8 +2042,13 @@ struct Pass {
     F3 f2, f3, bh0, bh1, da0;
     {
       const F3 w0 = bw2(0), w1 = bw2(1), w2 = bw2(2), w3 = bw2(3);
-      using PL = Plan<0, 11, 14, 11, 17, 11, 17, 24, 6>;
-      static_assert(PL::reg(7) < 12 && PL::reg(21) < 18, "d2b's split before its MFMAs");
+      // d2b's split (K-step 0 in 0 .. 10, 1 in 11 .. 16), the d2a image (0 2 .. 10, slot 1: the d3
+      // reads are issued) and the d2b image (12 14 .. 22, slot 2: the h2b reads are issued), the h1
+      // image reads (1 .. 11), d2a's first reads (13 15 17)
+      using PL = Plan<0, 11, 8, 11, 17, 8, 0, 12, 6, 12, 24, 6, 1, 7, 3, 7, 13, 3, 13, 19, 3>;
+      static_assert(PL::reg(7) < 12 && PL::reg(15) < 18, "d2b's split before its MFMAs");
+      static_assert(PL::reg(7) < PL::reg(22) && PL::reg(15) < PL::reg(25) && PL::reg(21) < PL::reg(34),
+                    "image halves after their splits, reads after the stores");
       weave<24, PL>(
           [&](auto kc) {
             constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
@@ -2011,21 +2068,23 @@ struct Pass {
             };
             if constexpr (U < 8) {
               split_d2b(0, U);
-            } else if constexpr (U < 11) {  // the h1 image (slot 2: the h2a reads are issued)
-              img_write_pt(imw + O_IM2, h1s[0], h1s[1], U - 8);
+            } else if constexpr (U < 16) {
+              split_d2b(1, U - 8);
+            } else if constexpr (U < 22) {  // the d2a image (slot 1)
+              constexpr int V = U - 16;
+              img_write_h(imw, V < 3 ? f0 : f1, V % 3, V / 3);
               lds_order();
-            } else if constexpr (U < 14) {
-              tr_pt(imr + O_IM2, DU, U - 11, bh0);
-            } else if constexpr (U < 22) {
-              split_d2b(1, U - 14);
-            } else if constexpr (U < 25) {
-              tr_pt(imr + O_IM2 + RS, DU, U - 22, bh1);
+            } else if constexpr (U < 28) {  // the d2b image (slot 2)
+              constexpr int V = U - 22;
+              img_write_h(imw + O_IM2, V < 3 ? f2 : f3, V % 3, V / 3);
               lds_order();
-            } else if constexpr (U < 28) {  // the d2a image (slot 1: the h2b reads are issued)
-              img_write_pt(imw, f0, f1, U - 25);
-              lds_order();
+            } else if constexpr (U < 31) {  // the h1 image (slot 3, written in layer 2)
+              tr_pt(imr + O_IM3, DU, U - 28, bh0);
+            } else if constexpr (U < 34) {
+              tr_pt(imr + O_IM3 + RS, DU, U - 31, bh1);
             } else {
-              tr_pt(imr, DU, U - 28, da0);
+              tr_pt(imr, DU, U - 34, da0);
+              lds_order();
             }
           });
     }
@@ -2034,8 +2093,13 @@ struct Pass {
     F3 a0, a1;
     {
       F3 da1, db0, db1, e0, e1;
-      using PL = Plan<0, 5, 6, 5, 11, 6, 11, 35, 33>;
-      static_assert(PL::reg(2) < 6 && PL::reg(8) < 12 && PL::reg(11) < 18, "image reads before their MFMAs");
+      // the d2 reads (0 .. 8), d1's mask (2 .. 9, after block C's last MFMA has landed) and split
+      // (10 .. 25), the d1 image (19 21 23 | 27 29 31, slot 1: the d2a reads are issued), dW1's
+      // operand reads (32 .. 35)
+      using PL = Plan<0, 9, 9, 2, 10, 8, 10, 26, 16, 19, 25, 3, 27, 33, 3, 32, 36, 6>;
+      static_assert(PL::reg(2) < 6 && PL::reg(5) < 12 && PL::reg(8) < 18, "image reads before their MFMAs");
+      static_assert(PL::reg(24) < PL::reg(33) && PL::reg(32) < PL::reg(36) && PL::reg(38) < PL::reg(39),
+                    "image halves after their splits, reads after the stores");
       weave<36, PL>(
           [&](auto kc) {
             constexpr int K = decltype(kc)::value, P = K % 6, T = K / 6;
@@ -2051,24 +2115,22 @@ struct Pass {
             if constexpr (U < 3) {
               tr_pt(imr + RS, DU, U, da1);
               lds_order();
-            } else if constexpr (U < 6) {  // the d2b image (slot 2: the h1 reads are issued)
-              img_write_pt(imw + O_IM2, f2, f3, U - 3);
-              lds_order();
+            } else if constexpr (U < 6) {
+              tr_pt(imr + O_IM2, DU, U - 3, db0);
             } else if constexpr (U < 9) {
-              tr_pt(imr + O_IM2, DU, U - 6, db0);
-            } else if constexpr (U < 12) {
-              tr_pt(imr + O_IM2 + RS, DU, U - 9, db1);
-            } else if constexpr (U < 20) {  // d1 masked by h1 > 0
-              mask2(d1, h1, 2 * (U - 12));
-            } else if constexpr (U < 36) {  // d1's split -> e0, e1
-              constexpr int V = U - 20, st = V / 8, q = (V % 8) / 2;
+              tr_pt(imr + O_IM2 + RS, DU, U - 6, db1);
+            } else if constexpr (U < 17) {  // d1 masked by h1 > 0
+              mask2(d1, h1, 2 * (U - 9));
+            } else if constexpr (U < 33) {  // d1's split -> e0, e1
+              constexpr int V = U - 17, st = V / 8, q = (V % 8) / 2;
               float v[8];
 #pragma unroll
               for (int e = 0; e < 8; e++) v[e] = d1[8 * st + e];
               if constexpr (V % 2 == 0) split_l1(v, q, st ? e1 : e0, rs);
               else split_l2(q, st ? e1 : e0, rs);
-            } else if constexpr (U < 39) {  // the d1 image (slot 1: the d2a reads are issued)
-              img_write_pt(imw, e0, e1, U - 36);
+            } else if constexpr (U < 39) {  // the d1 image (slot 1)
+              constexpr int V = U - 33;
+              img_write_h(imw, V < 3 ? e0 : e1, V % 3, V / 3);
               lds_order();
             } else if constexpr (U < 42) {  // dW1's A operands: 16x16x32 transposed reads
               tr_pt(imr16, DU, U - 39, a0);
@@ -2193,16 +2255,17 @@ __device__ __forceinline__ void adv_norm(const double *stats, double m_global, f
 // else the lanes re-read logp_old: the same instruction count either way).
 template <int KIND, class G>
 __device__ __forceinline__ void prefetch_g(float *slot, const float *X, int nin, const float *ret, const float *V,
-                                           const float *act, const float *lp, int64_t row0, int l) {
-  const v4i rx = rsrc_v(X + row0 * nin, 32 * nin * 4);
+                                           const float *act, const float *lp, int64_t row0, int l, int64_t M) {
+  const uint32_t rows = tile_rows(M, row0);
+  const v4i rx = rsrc_v(X + row0 * nin, rows * nin * 4);
 #pragma unroll
   for (int c = 0; c < G::XPIECES; c++) dma16(rx, slot + G::IN_X + 256 * c, 1024 * c + 16 * l);
   const uint32_t vo = 4 * (l & 31);
-  if (l < 32) dma4(rsrc_v(ret + row0, 128), slot + G::IN_S0, vo);
+  if (l < 32) dma4(rsrc_v(ret + row0, 4 * rows), slot + G::IN_S0, vo);
   if (KIND != K_CRITIC) {
-    if (l >= 32) dma4(rsrc_v(V + row0, 128), slot + G::IN_S0, vo);
-    if (l < 32) dma4(rsrc_v(lp + row0, 128), slot + G::IN_S1, vo);
-    if (l >= 32) dma4(rsrc_v((act ? act : lp) + row0, 128), slot + G::IN_S1, vo);
+    if (l >= 32) dma4(rsrc_v(V + row0, 4 * rows), slot + G::IN_S0, vo);
+    if (l < 32) dma4(rsrc_v(lp + row0, 4 * rows), slot + G::IN_S1, vo);
+    if (l >= 32) dma4(rsrc_v((act ? act : lp) + row0, 4 * rows), slot + G::IN_S1, vo);
   }
 }
 template <int KIND, class G>
@@ -2233,9 +2296,10 @@ __device__ __forceinline__ void load_sync_g(float *slot, const float *X, int nin
 // critic / actor launch, profiles/r04_x3_probe/ab_pf2.txt.)
 template <int KIND, class G>
 __device__ __forceinline__ void prefetch_any(const WaveSlot<G> &ws, float *slot, int64_t row0, const float *X, int nin,
-                                             const float *ret, const float *V, const float *act, const float *lp_old) {
-  if constexpr (G::NIC == NIN_CONT) prefetch_tile<KIND, LY>(slot, X, ret, V, act, lp_old, row0, ws.l);
-  else prefetch_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, ws.l);
+                                             const float *ret, const float *V, const float *act, const float *lp_old,
+                                             int64_t M) {
+  if constexpr (G::NIC == NIN_CONT) prefetch_tile<KIND, LY>(slot, X, ret, V, act, lp_old, row0, ws.l, M);
+  else prefetch_g<KIND, G>(slot, X, nin, ret, V, act, lp_old, row0, ws.l, M);
 }
 // The first tile's LDS-DMA, issued by the kernel before it stages the weights (its own slot is
 // disjoint from the weight images), so the HBM latency of the first inputs overlaps the staging;
@@ -2244,7 +2308,7 @@ template <int KIND, class G>
 __device__ __forceinline__ void prefetch_first(const WaveSlot<G> &ws, int64_t gw, int64_t M, const float *X, int nin,
                                                const float *ret, const float *V, const float *act,
                                                const float *lp_old) {
-  if (gw < uniform_i64(M / 32)) prefetch_any<KIND, G>(ws, ws.inb, gw * 32, X, nin, ret, V, act, lp_old);
+  if (gw < uniform_i64(M / 32)) prefetch_any<KIND, G>(ws, ws.inb, gw * 32, X, nin, ret, V, act, lp_old, M);
 }
 
 template <int KIND, class G, class Body>
@@ -2254,7 +2318,7 @@ __device__ __forceinline__ void tile_loop(const WaveSlot<G> &ws, int64_t gw, int
   const int64_t ntiles = uniform_i64((M + 31) / 32), nfull = uniform_i64(M / 32);
   constexpr bool FIXED = G::NIC == NIN_CONT;  // the 13-input heads: the f32 path's slot loaders
   auto prefetch = [&](float *slot, int64_t row0) {
-    prefetch_any<KIND, G>(ws, slot, row0, X, nin, ret, V, act, lp_old);
+    prefetch_any<KIND, G>(ws, slot, row0, X, nin, ret, V, act, lp_old, M);
   };
   int cb = 0;
   MHPPO_MARK(0);
@@ -2307,9 +2371,9 @@ constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3
 #ifndef MHPPO_X3_CRIT
 // the 13-input critic pass: bits 0-1 = forward fragments held in registers (1 W2, 2 W3), bit 2 =
 // dW4 in registers, bit 3 = DH2F + XCE ordering (A/B builds override)
-// 12: dW4 in registers, DH2F + XCE, no forward fragments held (the hand-placed passes need those
-// registers; the phase-by-phase pass's best was 13: W2's forward fragments held, ab_crit.txt)
-#define MHPPO_X3_CRIT 12
+// 13: dW4 in registers, DH2F + XCE, W2's forward fragments held (the hand-placed passes have the
+// registers since the forward writes the h images: 466 VGPRs; -2.1 % vs 12, profiles/r05_x3/ab.txt)
+#define MHPPO_X3_CRIT 13
 #endif
 constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
 constexpr int X3_CRIT_HB = 3 & ~((MHPPO_X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
@@ -2317,9 +2381,9 @@ constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 #ifndef MHPPO_X3_ACT
 // the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
 // fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE (A/B overrides)
-// 60: both backward fragments held, dW4 in registers, DH2F + XCE, no forward fragments (the hand-placed
-// passes spill with them; the phase-by-phase pass's best was 62: W3's held, ab_act.txt / ab_act2.txt)
-#define MHPPO_X3_ACT 60
+// 61: both backward fragments held, dW4 in registers, DH2F + XCE, W2's forward fragments held (485
+// VGPRs since the forward writes the h images; -1.5 % vs 60, profiles/r05_x3/ab.txt; W3's too spill)
+#define MHPPO_X3_ACT 61
 #endif
 constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
 constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
@@ -2334,6 +2398,9 @@ constexpr int X3_CC_HF = MHPPO_X3_CC & 3, X3_CA_HF = MHPPO_X3_CA & 3;
 #define MHPPO_X3_SCH 1  // the 13-input single-net passes with the hand-placed backward (A/B builds override)
 #endif
 constexpr bool X3_SCH = MHPPO_X3_SCH;
+namespace x3 {
+using G13P = std::conditional_t<X3_SCH, G13S, G13>;  // the 13-input single-net passes' geometry
+}
 constexpr bool X3_CC_W4R = MHPPO_X3_CC & 4, X3_CC_ORD = MHPPO_X3_CC & 8, X3_CA_ORD = MHPPO_X3_CA & 8;
 template <int KIND, class G>
 __global__ void __launch_bounds__(64 * x3::WAVES)
@@ -2620,8 +2687,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
                      n_in, M, ret, value, act, logp_old, stats, counts, m_global, out_mean, out_std,                 \
                      reinterpret_cast<double *>(wk.g), wk.d)
     if (split) {
-      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, G13);
-      else X3_LAUNCH(K_CONT, G13);
+      if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, G13P);
+      else X3_LAUNCH(K_CONT, G13P);
     } else if (n_in <= 15) {
       if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV16);
       else X3_LAUNCH(K_CHOICE, GC16);

@@ -21,6 +21,8 @@ PH_SCH = {1: "tile inputs wait", 2: "layer 1 (+h1 s0 split)", 3: "layer 2 (+payl
 PH_OLD = {1: "tile inputs wait", 2: "layer 1", 3: "layer 2", 4: "layer 3", 5: "loss + dW4/dB3 sums",
           6: "dW3", 7: "dH2 + masks + dB2 sums", 8: "dW2 + dH1", 9: "dW1"}
 PH = PH_OLD if os.environ.get("X3_PHASES_OLD") else PH_SCH
+if os.environ.get("X3_PHASES_ALL"):  # masked-mark builds: every slot, by number
+    PH = {k: f"slot {k}" for k in range(1, 14)}
 M = 10485760
 torch.manual_seed(0)
 actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
