@@ -159,6 +159,16 @@ typedef struct mhppo_rollout_bufs {
                            (mhppo_rollout_policy_part / _sample_env_part); rows then needs
                            N*S*P + 2 + 2 (parts + 1) entries */
     int32_t reserved;
+    int32_t *rec_of;    /* optional [N*S + N + 1] (NULL: record index = segment index): the compact
+                           record layout.  mhppo_rollout_begin fills it from exist: segment s = env*S
+                           + slot gets record rec_of[s] = its rank among the existing segments, or -1,
+                           and rec_of[N*S + e] = the existing segments before env e (e = 0 .. N);
+                           every per-step record of segment s (obs_c row, act, logp, rew) is then
+                           stored at record rec_of[s] of step t (obs_c[t][rec_of[s]], ...), and none
+                           for rec_of[s] = -1, so the present segments' records are contiguous and
+                           absent ones cost no stores (and share no cache line with present ones
+                           for mhppo_bucket_scatter, whose pos / bucket are then per record).  With
+                           one pedestrian (P == 1) feat_c must be obs_c[t] (the in-place record). */
 } mhppo_rollout_bufs;
 /* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
  * instead of the MFMA kernel; both are bit-identical (A/B and tests) */

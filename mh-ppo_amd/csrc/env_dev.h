@@ -39,7 +39,7 @@ namespace mhppo {
 // wave total to g_timing[14] (max) and counts the wave in g_timing[15]; tools/env_phases.py / train_phases.py read them.  Loads are
 // asynchronous, so a phase is charged with the wait for the data it first consumes.
 #if defined(MHPPO_TIMING) && defined(__HIP_DEVICE_COMPILE__)
-static __device__ unsigned long long g_timing[16];
+static __device__ unsigned long long g_timing[32];  // [16 + k]: the slowest wave's phase k
 // per-wave accumulators in LDS (one global atomic per phase and wave, at MHPPO_MARK_FLUSH)
 __device__ __forceinline__ unsigned long long *timing_slots() {
   // [wave][phase 1..14 at 1..14, last stamp at 15]: 2 KB, within the train kernel's LDS slack
@@ -71,7 +71,10 @@ __device__ __forceinline__ void timing_flush() {
   if ((threadIdx.x & 63) == 0) {
     unsigned long long tot = 0;
     for (int q = 1; q < 14; q++) {
-      if (a[q]) atomicAdd(&g_timing[q], a[q]);
+      if (a[q]) {
+        atomicAdd(&g_timing[q], a[q]);
+        atomicMax(&g_timing[16 + q], a[q]);
+      }
       tot += a[q];
     }
     atomicMax(&g_timing[14], tot);  // the slowest wave's phases 1-13 (a launch lasts as long as it)
@@ -81,7 +84,7 @@ __device__ __forceinline__ void timing_flush() {
 #define MHPPO_MARK(k) ::mhppo::timing_mark(k)
 #define MHPPO_MARK_FLUSH() ::mhppo::timing_flush()
 #elif defined(MHPPO_TIMING) && defined(__HIP__)
-static __device__ unsigned long long g_timing[16];
+static __device__ unsigned long long g_timing[32];
 #define MHPPO_MARK(k)
 #define MHPPO_MARK_FLUSH()
 #else
@@ -482,6 +485,10 @@ __device__ __forceinline__ void store_obs_wave(float *obs, int e, int N) {
 // writes the dynamic fields back.  With one env
 // per lane and 65 536 envs the GPU holds one wave per SIMD, so the in-place HBM view
 // serialises ~100 dependent memory round trips per step; this view needs ~3.
+#ifndef MHPPO_RNG_WIN
+#define MHPPO_RNG_WIN 16  // words of the register view's RNG window (A/B builds override)
+#endif
+static_assert(MHPPO_RNG_WIN <= MT_PAD, "the window's unconsumed tail stays inside the allocation");
 template <int V, int NC, int NAV, int NP>
 struct EnvR {
   static constexpr int VAR = V;
@@ -493,7 +500,7 @@ struct EnvR {
   const Cfg &c;
   const Bufs &b;
   int e;
-  RngT<16> rng;
+  RngT<MHPPO_RNG_WIN> rng;
   double cross, cl;
   mutable double car_[C_NF][NC];
   mutable double ped_[P_NF][NP];

@@ -111,6 +111,17 @@ __global__ void __launch_bounds__(TPB)
 
 // -------------------------------------------------------------- step
 // one lane per (env, slot, ped): obs_car_ped features + cross/wait actor
+// Record index of segment s = env * nS + slot in the time-major records: B.rec_of[s] in the
+// compact layout (-1: the segment stores no record), else s (include/mhppo.h mhppo_rollout_bufs)
+__device__ __forceinline__ int64_t rec_index(const mhppo_rollout_bufs &B, int64_t s) {
+  return B.rec_of ? (int64_t)B.rec_of[s] : s;
+}
+// feat_c row of policy row r = (env, slot, ped): with one pedestrian and the compact layout, feat_c
+// is the step's record obs_c[t] and row r its segment's record (-1: none)
+__device__ __forceinline__ int64_t feat_row(const mhppo_rollout_bufs &B, int P, int64_t r) {
+  return P == 1 ? rec_index(B, r) : r;
+}
+
 template <int V>
 __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp mw, mhppo_rollout_bufs B) {
   extern __shared__ float lds[];
@@ -129,9 +140,12 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
   const float *o = B.obs + e * L.obs_dim;
   float f[NF_C];
   float ex = obs_car_ped(o, L, i, p, f);
-  float *fo = B.feat_c + r * NF_C;
+  const int64_t fr = feat_row(B, c.P, (int64_t)r);
+  if (fr >= 0) {
+    float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
-  for (int k = 0; k < NF_C; k++) fo[k] = f[k];
+    for (int k = 0; k < NF_C; k++) fo[k] = f[k];
+  }
   if (L.scalable && ex == 0.0f) return;  // `if exist:` gate of the scalable driver (:439)
   // action_d = 2*a - 1; cross head when action_d <= 0 (:440-445)
   bool wait = (2 * B.a_d[r] - 1) > 0;
@@ -179,9 +193,12 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
   const float *o = B.obs + (size_t)e * L.obs_dim;
   float f[NF_C];
   float ex = obs_car_ped(o, L, i, p, f);
-  float *fo = B.feat_c + (size_t)r * NF_C;
+  const int64_t fr = feat_row(B, c.P, r);
+  if (fr >= 0) {
+    float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
-  for (int q = 0; q < NF_C; q++) fo[q] = f[q];
+    for (int q = 0; q < NF_C; q++) fo[q] = f[q];
+  }
   if (L.scalable && ex == 0.0f) return;  // `if exist:` gate of the scalable driver (:439)
   const float out = mlp_forward13_rows(head ? Ww : Wc, f);
   // Model_PPO type 1: tanh(x) * std + mean (:87-89), two roundings
@@ -409,8 +426,9 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
     r_nxt = r_2;
     ok_nxt = ok_2;
     raw_cur = raw_nxt;
-    if (valid && kh == 0) {
-      float *fo = B.feat_c + (size_t)r * NF_C;
+    const int64_t fr = valid ? feat_row(B, c.P, r) : -1;
+    if (fr >= 0 && kh == 0) {
+      float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
       for (int q = 0; q < NF_C; q++) fo[q] = f[q];
     }
@@ -479,6 +497,66 @@ __global__ void __launch_bounds__(TPB) k_head_place(const int32_t *a_d, int R, c
   }
 }
 
+// The compact record layout (mhppo_rollout_bufs.rec_of): rank[s] = the number of flagged
+// segments before s (flag[s] != 0), -1 for an unflagged one.  Two passes as the head lists:
+// per-block counts, then every block sums the counts before it and ranks its rows by wave prefix.
+__global__ void __launch_bounds__(TPB) k_flag_count(const uint8_t *flag, int R, int32_t *cnt) {
+  __shared__ int wsum[TPB / 64];
+  const int r = blockIdx.x * TPB + threadIdx.x;
+  const uint64_t m = __ballot(r < R && flag[r] != 0);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < TPB / 64; w++) s += wsum[w];
+    cnt[blockIdx.x] = s;
+  }
+}
+__global__ void __launch_bounds__(TPB) k_flag_rank(const uint8_t *flag, int R, const int32_t *cnt, int nblk,
+                                                   int32_t *rank, int S, int32_t *pre) {
+  __shared__ int red[TPB];
+  __shared__ int wsum[TPB / 64];
+  int before = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x && b < nblk; b += TPB) before += cnt[b];
+  red[threadIdx.x] = before;
+  __syncthreads();
+  for (int st = TPB / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  const int r = blockIdx.x * TPB + threadIdx.x;
+  const bool f = r < R && flag[r] != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t m = __ballot(f);
+  if (lane == 0) wsum[w] = __popcll(m);
+  __syncthreads();
+  int wc = 0;
+  for (int q = 0; q < w; q++) wc += wsum[q];
+  const uint64_t below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
+  const int nbefore = red[0] + wc + __popcll(below);  // flagged segments before r
+  if (r < R) rank[r] = f ? nbefore : -1;
+  // pre[g] = flagged segments before segment g S (g = 0 .. R / S): per-group record ranges
+  if (r < R && r % S == 0) pre[r / S] = nbefore;
+  if (r == R - 1) pre[R / S] = nbefore + (f ? 1 : 0);
+}
+
+// The compact layout's step records of one full wave (the scalable env): its 64 envs' present
+// segments are the records [R0, R0 + K) (R0 = the existing segments before its first env,
+// mhppo_rollout_bufs.rec_of[N S + e]); each lane puts its slots' act / logp / rew at (record - R0)
+// in the wave's LDS run, and the wave writes the run as lane-contiguous stores.  (Stored per lane,
+// the records' 4- and 8-byte values land scattered over the run and leave as partial lines:
+// +2 % HBM bytes and +4 % time for the step kernel at config 4.)
+template <int CNS>
+struct RecStage {
+  float act[64 * CNS], logp[64 * CNS];
+  double rew[64 * CNS];
+};
+template <int CNS>
+__device__ __forceinline__ RecStage<CNS> *rec_stage_wave() {
+  __shared__ RecStage<CNS> st[TPB / 64];
+  return &st[(threadIdx.x >> 6) & (TPB / 64 - 1)];
+}
+
 // one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min.
 // All of this lane's rollout inputs are read before any buffer write so the loads
 // issue as one batch; EV is the generic or the register env view.
@@ -501,9 +579,31 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   // feat_c verbatim: the host points feat_c at obs_c[t] for the policy step (rollout.py
   // collect) and nothing is copied here.  Otherwise each slot's selected row is copied.
   const bool feat_in_place = B.feat_c == B.obs_c + (size_t)t * c.N * S * NF_C && P == 1;
-  // compile-time S multiple of 4: the step's act/logp/rew/ep_min records go out as vectors
+  // compile-time S multiple of 4: the step's act/logp/rew/ep_min records go out as vectors (the
+  // identity record layout; the compact one stores each present segment's record at its index)
   constexpr bool REC_VEC = EV::CNS > 0 && EV::CNS % 4 == 0;
+  const bool vec = REC_VEC && !B.rec_of;
+  // the compact layout on a full wave of the register-view step: records staged per wave (RecStage)
+  constexpr bool STAGE = V == V_SCALABLE && REC_VEC && !REG_OUT;
+  const int lane = threadIdx.x & 63;
+  const int e0 = __builtin_amdgcn_readfirstlane(e - lane);
+  const bool staged = STAGE && B.rec_of && e0 + 64 <= c.N;
+  int R0 = 0, K = 0;
+  if (staged) {  // the wave's record run (uniform loads, issued with the other inputs)
+    R0 = B.rec_of[(size_t)c.N * S + e0];
+    K = B.rec_of[(size_t)c.N * S + e0 + 64] - R0;
+  }
+  // this env's records: its present slots (exist, set by mhppo_rollout_begin) in slot order from
+  // the env's first record (one prefix load and the S exist bytes, not S rank loads)
+  int64_t rbase = 0;
+  uint32_t emask = 0;
+  if (B.rec_of) {
+    rbase = B.rec_of[(size_t)c.N * S + e];
+    MHPPO_UNROLL
+    for (int i = 0; i < S; i++) emask |= (uint32_t)(B.exist[(size_t)e * S + i] != 0) << i;
+  }
   float av[REC_VEC ? EV::CNS : 1], lv[REC_VEC ? EV::CNS : 1];
+  int64_t rix[EV::CNS > 0 ? EV::CNS : EV::MAXAV];  // this step's record of each slot (-1: none)
   MHPPO_UNROLL
   for (int i = 0; i < S; i++) {
     size_t row0 = ((size_t)e * S + i) * P;
@@ -524,15 +624,17 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     if (loc != loc && B.status) atomicOr(B.status, 2u);  // MultivariateNormal raises on a NaN loc
     float z = eps[(size_t)e * S + i];
     float a = loc + MVN_L * z;
-    const size_t bt = ((size_t)t * c.N + e) * S + i;  // time-major records [T][N][S]
-    if constexpr (REC_VEC) {
+    rix[i] = !B.rec_of ? (int64_t)e * S + i
+                       : (((emask >> i) & 1u) ? rbase + __builtin_popcount(emask & ((1u << i) - 1u)) : -1);
+    const int64_t bt = (int64_t)t * c.N * S + rix[i];  // time-major records [T][N S]
+    if (REC_VEC && (vec || staged)) {
       av[i] = a;
       lv[i] = mvn_logp(a, loc);
-    } else {
+    } else if (rix[i] >= 0) {
       B.act[bt] = a;
       B.logp[bt] = mvn_logp(a, loc);
     }
-    if (!feat_in_place) {
+    if (!feat_in_place && rix[i] >= 0) {
       const float *fs = B.feat_c + (row0 + sel) * NF_C;
       float *fo = B.obs_c + bt * NF_C;
 #pragma unroll
@@ -544,10 +646,10 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     const int cp = EV::CNP == 1 ? 0 : B.closest[(size_t)e * S + i];
     act[S + i] = (double)(2 * B.a_d[row0 + cp] - 1);  // action_d_light (:423-424)
   }
-  if constexpr (REC_VEC) {  // this env's S records of step t are contiguous and 16-B aligned
+  if (REC_VEC && vec) {  // this env's S records of step t are contiguous and 16-B aligned
     const size_t b0 = ((size_t)t * c.N + e) * S;
 #pragma unroll
-    for (int q = 0; q < EV::CNS / 4; q++) {
+    for (int q = 0; q < (REC_VEC ? EV::CNS / 4 : 0); q++) {
       reinterpret_cast<float4 *>(B.act + b0)[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
       reinterpret_cast<float4 *>(B.logp + b0)[q] = make_float4(lv[4 * q], lv[4 * q + 1], lv[4 * q + 2], lv[4 * q + 3]);
     }
@@ -565,17 +667,46 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     double x = E.rl[i];
     epm[i] = (m != m) ? m : ((x != x) ? x : (x < m ? x : m));  // np.minimum: NaN-propagating
   }
-  if constexpr (REC_VEC) {
+  if constexpr (STAGE) {
+    if (staged) {
+      RecStage<EV::CNS> *st = rec_stage_wave<EV::CNS>();
+      MHPPO_UNROLL
+      for (int i = 0; i < S; i++) {
+        if (rix[i] >= 0) {
+          const int o = (int)(rix[i] - R0);
+          st->act[o] = av[i];
+          st->logp[o] = lv[i];
+          st->rew[o] = E.rw[i];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int64_t base = (int64_t)t * c.N * S + R0;
+      for (int j = lane; j < K; j += 64) {
+        B.act[base + j] = st->act[j];
+        B.logp[base + j] = st->logp[j];
+        B.rew[base + j] = st->rew[j];
+      }
+#pragma unroll
+      for (int q = 0; q < EV::CNS / 2; q++)
+        reinterpret_cast<double2 *>(B.ep_min + (size_t)e * S)[q] = make_double2(epm[2 * q], epm[2 * q + 1]);
+      MHPPO_MARK(10);
+      MHPPO_MARK_FLUSH();
+      return;
+    }
+  }
+  if (REC_VEC && vec) {
     const size_t b0 = ((size_t)t * c.N + e) * S;
 #pragma unroll
-    for (int q = 0; q < EV::CNS / 2; q++) {
+    for (int q = 0; q < (REC_VEC ? EV::CNS / 2 : 0); q++) {
       reinterpret_cast<double2 *>(B.rew + b0)[q] = make_double2(E.rw[2 * q], E.rw[2 * q + 1]);
       reinterpret_cast<double2 *>(B.ep_min + (size_t)e * S)[q] = make_double2(epm[2 * q], epm[2 * q + 1]);
     }
   } else {
     MHPPO_UNROLL
     for (int i = 0; i < S; i++) {
-      B.rew[((size_t)t * c.N + e) * S + i] = E.rw[i];
+      if (rix[i] >= 0) B.rew[(int64_t)t * c.N * S + rix[i]] = E.rw[i];
       B.ep_min[(size_t)e * S + i] = epm[i];
     }
   }
@@ -697,8 +828,9 @@ __global__ void __launch_bounds__(TPB)
     float f[NF_C + 1];
     const float ex = obs_car_ped_raw(raw_cur, f);
     f[NF_C] = 0.0f;
-    if (ok_cur && kh == 0) {
-      float *fo = B.feat_c + (size_t)r_cur * NF_C;
+    const int64_t fr = ok_cur ? feat_row(B, 1, r_cur) : -1;  // (the fused step: one pedestrian)
+    if (fr >= 0 && kh == 0) {
+      float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
       for (int q = 0; q < NF_C; q++) fo[q] = f[q];
     }
@@ -1251,8 +1383,15 @@ extern "C" int mhppo_debug_wave_times(unsigned long long *out) {  // [2 * 8192]:
 int mhppo_debug_timing(unsigned long long *out16) {
   CHECK_HIP(hipDeviceSynchronize());
   CHECK_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 16));
-  unsigned long long z[16] = {0};
+  unsigned long long z[32] = {0};
   CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)));
+  return MHPPO_OK;
+}
+// the per-phase slowest-wave cycles (g_timing[16 + k]); read before mhppo_debug_timing clears them
+int mhppo_debug_timing_max(unsigned long long *out16) {
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 16,
+                                sizeof(unsigned long long) * 16));
   return MHPPO_OK;
 }
 #endif
@@ -1288,6 +1427,15 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
     if (bufs->parts > 1) hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, s, c, bufs->rows, (int)bufs->parts);
   }
   size_t NS = (size_t)c.N * c.nS;
+  if (bufs->rec_of) {  // the compact record layout: present segments ranked in (env, slot) order
+    if (!bufs->exist) return set_error(MHPPO_EINVAL, "rec_of needs exist");
+    const int nblk = (int)grid_for(NS).x;
+    int32_t *cnt = reinterpret_cast<int32_t *>(scratch((nblk + 1) / 2));
+    if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+    hipLaunchKernelGGL(k_flag_count, grid_for(NS), dim3(TPB), 0, s, bufs->exist, (int)NS, cnt);
+    hipLaunchKernelGGL(k_flag_rank, grid_for(NS), dim3(TPB), 0, s, bufs->exist, (int)NS, cnt, nblk, bufs->rec_of,
+                       c.nS, bufs->rec_of + NS);
+  }
   hipLaunchKernelGGL(k_fill_f64, grid_for(NS), dim3(TPB), 0, s, bufs->ep_min, NS, 0.0);  // np.array([0.]*S) (:383)
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;

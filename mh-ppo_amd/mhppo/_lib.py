@@ -40,7 +40,7 @@ class RolloutBufs(ctypes.Structure):
     _fields_ = [("feat_d", P), ("probs_d", P), ("logp_d", P), ("a_d", P), ("closest", P),
                 ("feat_c", P), ("out_c", P), ("obs", P), ("obs_c", P), ("act", P), ("logp", P),
                 ("rew", P), ("ep_min", P), ("exist", P), ("rows", P), ("T", I32),
-                ("flags", I32), ("status", P), ("parts", I32), ("reserved", I32)]
+                ("flags", I32), ("status", P), ("parts", I32), ("reserved", I32), ("rec_of", P)]
 
 
 class EvalBufs(ctypes.Structure):

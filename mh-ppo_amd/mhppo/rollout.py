@@ -16,6 +16,7 @@ the GLOBAL env id, so a sharded run draws the same noise per env as a single
 GPU.  In parity mode callers pass the reference's recorded draws instead.
 """
 import ctypes
+import os
 
 import torch
 
@@ -26,10 +27,27 @@ _CTR_STEP = 1 << 40  # counter stride between time steps (global env*slot index 
 
 
 class RolloutBatch:
-    """Views of one iteration's rollout buffers (all on the env's device)."""
+    """Views of one iteration's rollout buffers (all on the env's device).  With the compact
+    record layout (rec_of set: the scalable env, whose absent car slots store no records) obs_c /
+    act / logp / rew are gathered from the time-major records on first access, absent segments
+    zero."""
+
+    _REC = ("obs_c", "act", "logp", "rew")
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
+
+    def __getattr__(self, name):
+        if name not in RolloutBatch._REC or self.__dict__.get("rec_of") is None:
+            raise AttributeError(name)
+        N, S, T = self.N, self.S, self.T
+        ro = self.rec_of.long()
+        x = getattr(self, name + "_tm").reshape(T, N * S, -1).index_select(1, ro.clamp_min(0))
+        x = torch.where((ro >= 0).reshape(1, -1, 1), x, torch.zeros((), dtype=x.dtype, device=x.device))
+        x = x.reshape(T, N, S, -1).permute(1, 2, 0, 3)
+        v = x if name == "obs_c" else x[..., 0]
+        self.__dict__[name] = v
+        return v
 
 
 # Envs per part below which the rollout runs as one chain (parts = 1): with fewer than ~256 waves of
@@ -94,6 +112,12 @@ class RolloutGPU:
         self.exist = z((N, S), torch.uint8)
         self.eps = z((self.T, N, S), f32)
         self.u = z((N, S, P), f32)
+        # the compact record layout (include/mhppo.h mhppo_rollout_bufs.rec_of) where car slots can
+        # be absent (the scalable env): absent segments store no records, present ones are
+        # contiguous (MHPPO_COMPACT_RECORDS=0: the identity layout)
+        self.compact = venv.variant == "scalable" and os.environ.get("MHPPO_COMPACT_RECORDS", "1") != "0"
+        self.rec_buf = z(N * S + N + 1, i32) if self.compact else None  # segment ranks | per-env prefix
+        self.rec_of = self.rec_buf[:N * S] if self.compact else None
         # the fused one-launch step (one pedestrian, compiled shapes): bit-identical to the two launches
         self.fused_ok = bool(_lib.lib().mhppo_rollout_fused_supported(venv.handle) == 1) and not valu_policy
         self.fused = self.fused_ok and (default_fused() if fused is None else bool(fused))
@@ -108,6 +132,7 @@ class RolloutGPU:
                      "logp", "rew", "ep_min", "exist", "rows", "status"):
             setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
         b.T = self.T
+        b.rec_of = ctypes.c_void_p(self.rec_buf.data_ptr()) if self.compact else None
         # policy step on the VALU kernel instead of the MFMA one (bit-identical; A/B and tests)
         b.flags = 1 if valu_policy else 0  # MHPPO_ROLLOUT_VALU_POLICY
         b.parts = self.parts
@@ -285,10 +310,11 @@ class RolloutGPU:
             self._parts_loop(L, mx, mw, nparts, torch.cuda.current_stream(dev))
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued
         # obs_c/act/logp/rew: [N, S, T(, 13)] views of the time-major buffers (*_tm)
+        views = {} if self.compact else dict(obs_c=self.obs_c.permute(1, 2, 0, 3), act=self.act.permute(1, 2, 0),
+                                             logp=self.logp.permute(1, 2, 0), rew=self.rew.permute(1, 2, 0))
         return RolloutBatch(feat_d=self.feat_d, probs_d=self.probs_d, logp_d=self.logp_d, a_d=self.a_d,
-                            closest=self.closest, obs_c=self.obs_c.permute(1, 2, 0, 3), act=self.act.permute(1, 2, 0),
-                            logp=self.logp.permute(1, 2, 0), rew=self.rew.permute(1, 2, 0), obs_c_tm=self.obs_c,
-                            act_tm=self.act, logp_tm=self.logp, rew_tm=self.rew, ep_min=self.ep_min,
+                            closest=self.closest, **views, obs_c_tm=self.obs_c,
+                            act_tm=self.act, logp_tm=self.logp, rew_tm=self.rew, ep_min=self.ep_min, rec_of=self.rec_of,
                             exist=self.exist, N=self.N, S=self.S, P=self.P, T=self.T)
 
 
@@ -369,6 +395,10 @@ def bucket_segments(batch, fix_bucket=False, status=None):
     w0 = torch.div(cc[-1] + 3, 4, rounding_mode="floor") * 4
     pos = torch.where(cross, cc - 1, torch.where(wait, w0 + cw - 1, -1))
     bucket = torch.zeros(NS, dtype=torch.int8, device=pos.device)
+    rec_of = getattr(batch, "rec_of", None)
+    if rec_of is not None:  # the compact layout: the scatter's positions are per record
+        idx = torch.where(rec_of >= 0, rec_of, NS).long()
+        pos = torch.full((NS + 1,), -1, dtype=pos.dtype, device=pos.device).scatter_(0, idx, pos)[:NS]
     (both,) = scatter_positions(pos, bucket, (NS + 3,), NS, T, batch.obs_c_tm, batch.act_tm, batch.logp_tm, ret,
                                 batch.rew_tm)
     seg_all = torch.nonzero_static(exist, size=NS, fill_value=0).squeeze(1)

@@ -9,6 +9,7 @@ for v in "$@"; do
     echo "== $v $cfg"
     MHPPO_LIB=$lib ROLLOUT_CFG="$cfg" timeout -k 10 120 python tools/env_steps.py > gpurun_out/ab_env_step.txt 2>&1 || exit 1
     grep "mean" gpurun_out/ab_env_step.txt
+    python3 -c "import re,sys;v=[float(m.group(2)) for m in re.finditer(r'step +(\\d+): +([\\d.]+) us', open(sys.argv[1]).read()) if 2<=int(m.group(1))<=18];print('  steps 2-18 mean %.1f us, max %.1f' % (sum(v)/len(v), max(v)))" gpurun_out/ab_env_step.txt
   done
 done
 exit 0

@@ -21,6 +21,9 @@ PHASES = {1: "MT refill (wave)", 2: "env state load (EnvR)", 3: "select + MVN ac
 
 
 def per_step(algo, fn, buf):
+    fmax = _lib.lib().mhppo_debug_timing_max
+    fmax.restype, fmax.argtypes = ctypes.c_int32, [ctypes.c_void_p]
+    bmax = (ctypes.c_uint64 * 16)()
     """Phase cycles per wave of every step of one rollout (the collect loop of RolloutGPU.collect,
     synchronised and read back after each env-step launch)."""
     L = _lib.lib()
@@ -44,12 +47,14 @@ def per_step(algo, fn, buf):
             fn(buf)  # clears
             _lib.check(L.mhppo_rollout_sample_env(ro.venv.handle, _lib.ptr(ro.eps[t]), t, ctypes.byref(ro._bufs), st))
             torch.cuda.synchronize()
+            fmax(bmax)
             fn(buf)
             w = max(buf[15], 1)
-            rows.append(([buf[k] / w for k in PHASES], buf[14]))
-    print("step " + " ".join(f"{PHASES[k][:10]:>10s}" for k in PHASES) + "  (mean wave)   slowest wave")
-    for t, (r, mx) in enumerate(rows):
+            rows.append(([buf[k] / w for k in PHASES], buf[14], [bmax[k] for k in PHASES]))
+    print("step " + " ".join(f"{PHASES[k][:10]:>10s}" for k in PHASES) + "  (mean wave / slowest wave per phase)")
+    for t, (r, mx, pm) in enumerate(rows):
         print(f"{t:4d} " + " ".join(f"{x:10.0f}" for x in r) + f"  total {sum(r):8.0f}  max {mx:8d}")
+        print("  max" + " ".join(f"{x:10d}" for x in pm))
 
 
 def main():
