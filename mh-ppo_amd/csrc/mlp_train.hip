@@ -2371,9 +2371,10 @@ constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3
 #ifndef MHPPO_X3_CRIT
 // the 13-input critic pass: bits 0-1 = forward fragments held in registers (1 W2, 2 W3), bit 2 =
 // dW4 in registers, bit 3 = DH2F + XCE ordering (A/B builds override)
-// 13: dW4 in registers, DH2F + XCE, W2's forward fragments held (the hand-placed passes have the
-// registers since the forward writes the h images: 466 VGPRs; -2.1 % vs 12, profiles/r05_x3/ab.txt)
-#define MHPPO_X3_CRIT 13
+// 15: dW4 in registers, DH2F + XCE, W2's and W3's forward fragments held (the hand-placed passes
+// have the registers since the forward writes the h images: 509 VGPRs; 12 -> 13 -2.1 %, 13 -> 15
+// -3.5 %, profiles/r05_x3/ab.txt, ab_hf3.txt)
+#define MHPPO_X3_CRIT 15
 #endif
 constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
 constexpr int X3_CRIT_HB = 3 & ~((MHPPO_X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
