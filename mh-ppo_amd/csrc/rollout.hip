@@ -443,57 +443,69 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
 // Head lists for k_policy_sorted / k_policy_mfma (stable: each list in row order).  Pass 1 counts the
 // cross rows of each 256-row block; pass 2 has every block sum the counts before it
 // (and all of them, for the wait list's base), then place its rows by wave prefix.
-__global__ void __launch_bounds__(TPB) k_head_count(const int32_t *a_d, int R, int32_t *cnt) {
-  __shared__ int wsum[TPB / 64];
+// present: optional [R / P] segment flags (the compact record layout): rows of absent car slots join
+// neither list — the policy skips them (their outputs are never read and they store no record).
+// cnt[2 b] / cnt[2 b + 1]: block b's cross / wait rows.
+__global__ void __launch_bounds__(TPB) k_head_count(const int32_t *a_d, int R, int32_t *cnt, const uint8_t *present,
+                                                    int P) {
+  __shared__ int wsum[2][TPB / 64];
   const int r = blockIdx.x * TPB + threadIdx.x;
-  const bool cross = r < R && a_d[r] == 0;  // action_d = 2a - 1 <= 0 (:440-445)
-  const uint64_t m = __ballot(cross);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(m);
+  const bool valid = r < R && (!present || present[r / P]);
+  const bool cross = valid && a_d[r] == 0;  // action_d = 2a - 1 <= 0 (:440-445)
+  const uint64_t mc = __ballot(cross), mw = __ballot(valid && !cross);
+  if ((threadIdx.x & 63) == 0) {
+    wsum[0][threadIdx.x >> 6] = __popcll(mc);
+    wsum[1][threadIdx.x >> 6] = __popcll(mw);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 2) {
     int s = 0;
-    for (int w = 0; w < TPB / 64; w++) s += wsum[w];
-    cnt[blockIdx.x] = s;
+    for (int w = 0; w < TPB / 64; w++) s += wsum[threadIdx.x][w];
+    cnt[2 * blockIdx.x + threadIdx.x] = s;
   }
 }
 
 __global__ void __launch_bounds__(TPB) k_head_place(const int32_t *a_d, int R, const int32_t *cnt, int nblk,
-                                                    int32_t *rows) {
-  __shared__ int red[2][TPB];
-  __shared__ int wsum[TPB / 64];
-  int before = 0, total = 0;
+                                                    int32_t *rows, const uint8_t *present, int P) {
+  __shared__ int red[4][TPB];
+  __shared__ int wsum[2][TPB / 64];
+  int cb = 0, ct = 0, wb = 0, wt = 0;  // cross / wait rows before this block and in all
   for (int b = threadIdx.x; b < nblk; b += TPB) {
-    const int v = cnt[b];
-    total += v;
-    before += b < (int)blockIdx.x ? v : 0;
+    const int c = cnt[2 * b], w = cnt[2 * b + 1];
+    ct += c;
+    wt += w;
+    if (b < (int)blockIdx.x) cb += c, wb += w;
   }
-  red[0][threadIdx.x] = before;
-  red[1][threadIdx.x] = total;
+  red[0][threadIdx.x] = cb;
+  red[1][threadIdx.x] = ct;
+  red[2][threadIdx.x] = wb;
+  red[3][threadIdx.x] = wt;
   __syncthreads();
-  for (int s = TPB / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
+  for (int st = TPB / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st)
+      for (int k = 0; k < 4; k++) red[k][threadIdx.x] += red[k][threadIdx.x + st];
     __syncthreads();
   }
-  const int nc = red[1][0], cbase = red[0][0];
+  const int cbase = red[0][0], nc = red[1][0], wbase = red[2][0], nwt = red[3][0];
   const int r = blockIdx.x * TPB + threadIdx.x;
-  const bool valid = r < R;
+  const bool valid = r < R && (!present || present[r / P]);
   const bool cross = valid && a_d[r] == 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t m = __ballot(cross);
-  if (lane == 0) wsum[w] = __popcll(m);
+  const uint64_t mc = __ballot(cross), mw = __ballot(valid && !cross);
+  if (lane == 0) {
+    wsum[0][w] = __popcll(mc);
+    wsum[1][w] = __popcll(mw);
+  }
   __syncthreads();
-  int wc = 0;
-  for (int q = 0; q < w; q++) wc += wsum[q];
-  const uint64_t below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
-  const int ci = cbase + wc + __popcll(below);                  // cross rows before r
-  const int wi = (blockIdx.x * TPB + w * 64 + lane) - ci;        // wait rows before r
+  int wc = 0, ww = 0;
+  for (int q = 0; q < w; q++) wc += wsum[0][q], ww += wsum[1][q];
+  const uint64_t lt = lane ? ((1ull << lane) - 1) : 0ull;
+  const int ci = cbase + wc + __popcll(mc & lt);  // cross rows before r
+  const int wi = wbase + ww + __popcll(mw & lt);  // wait rows before r
   if (valid) rows[cross ? ci : nc + wi] = r;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     rows[R] = nc;
-    rows[R + 1] = R - nc;
+    rows[R + 1] = nwt;
   }
 }
 
@@ -1358,7 +1370,7 @@ __global__ void k_part_bounds(Cfg c, int32_t *rows, int nparts) {
     else hi = m;
   }
   rows[R + 2 + p] = lo;
-  lo = nc, hi = R;
+  lo = nc, hi = nc + rows[R + 1];  // the wait list (absent rows, if skipped, join neither list)
   while (lo < hi) {
     const int m = (lo + hi) >> 1;
     if (rows[m] < rb) lo = m + 1;
@@ -1418,14 +1430,6 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
   size_t shm = sizeof(float) * choice_lds_floats(c, actor_choice->n_in);
   if (shm > 160 * 1024) return set_error(MHPPO_EINVAL, "choice kernel LDS %zu B (obs_dim %d, dc %d)", shm, c.obs_dim, choice_dim(c));
   VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, *actor_choice, u, forced_a, *bufs);
-  if (bufs->rows) {  // head lists for k_policy_sorted (the choice is fixed for the episode)
-    const int nblk = (int)grid_for(R).x;
-    int32_t *cnt = reinterpret_cast<int32_t *>(scratch((nblk + 1) / 2));
-    if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
-    hipLaunchKernelGGL(k_head_count, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt);
-    hipLaunchKernelGGL(k_head_place, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt, nblk, bufs->rows);
-    if (bufs->parts > 1) hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, s, c, bufs->rows, (int)bufs->parts);
-  }
   size_t NS = (size_t)c.N * c.nS;
   if (bufs->rec_of) {  // the compact record layout: present segments ranked in (env, slot) order
     if (!bufs->exist) return set_error(MHPPO_EINVAL, "rec_of needs exist");
@@ -1435,6 +1439,18 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
     hipLaunchKernelGGL(k_flag_count, grid_for(NS), dim3(TPB), 0, s, bufs->exist, (int)NS, cnt);
     hipLaunchKernelGGL(k_flag_rank, grid_for(NS), dim3(TPB), 0, s, bufs->exist, (int)NS, cnt, nblk, bufs->rec_of,
                        c.nS, bufs->rec_of + NS);
+  }
+  if (bufs->rows) {  // head lists for k_policy_sorted (the choice is fixed for the episode)
+    const int nblk = (int)grid_for(R).x;
+    int32_t *cnt = reinterpret_cast<int32_t *>(scratch(nblk));
+    if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
+    // every row: a car slot absent at t = 0 (no record) can be present later in the episode, and its
+    // action then drives the env (skipping those rows diverged the scalable reference rollout)
+    const uint8_t *present = nullptr;
+    hipLaunchKernelGGL(k_head_count, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt, present, c.P);
+    hipLaunchKernelGGL(k_head_place, grid_for(R), dim3(TPB), 0, s, bufs->a_d, (int)R, cnt, nblk, bufs->rows, present,
+                       c.P);
+    if (bufs->parts > 1) hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, s, c, bufs->rows, (int)bufs->parts);
   }
   hipLaunchKernelGGL(k_fill_f64, grid_for(NS), dim3(TPB), 0, s, bufs->ep_min, NS, 0.0);  // np.array([0.]*S) (:383)
   CHECK_HIP(hipGetLastError());
