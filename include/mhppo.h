@@ -168,7 +168,9 @@ typedef struct mhppo_rollout_bufs {
                            for rec_of[s] = -1, so the present segments' records are contiguous and
                            absent ones cost no stores (and share no cache line with present ones
                            for mhppo_bucket_scatter, whose pos / bucket are then per record).  With
-                           one pedestrian (P == 1) feat_c must be obs_c[t] (the in-place record). */
+                           one pedestrian (P == 1) feat_c must be obs_c[t] (the in-place record).
+                           The scalable env only (the variant whose car slots can be absent):
+                           mhppo_rollout_begin returns MHPPO_EINVAL for another. */
 } mhppo_rollout_bufs;
 /* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
  * instead of the MFMA kernel; both are bit-identical (A/B and tests) */

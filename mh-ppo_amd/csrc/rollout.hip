@@ -113,13 +113,22 @@ __global__ void __launch_bounds__(TPB)
 // one lane per (env, slot, ped): obs_car_ped features + cross/wait actor
 // Record index of segment s = env * nS + slot in the time-major records: B.rec_of[s] in the
 // compact layout (-1: the segment stores no record), else s (include/mhppo.h mhppo_rollout_bufs)
+// The compact layout is the scalable env's only (the variant whose car slots can be absent;
+// mhppo_rollout_begin rejects rec_of for the others), so the other variants compile without it.
+template <int V>
+__device__ __forceinline__ const int32_t *rec_map(const mhppo_rollout_bufs &B) {
+  return V == V_SCALABLE ? B.rec_of : nullptr;
+}
+template <int V>
 __device__ __forceinline__ int64_t rec_index(const mhppo_rollout_bufs &B, int64_t s) {
-  return B.rec_of ? (int64_t)B.rec_of[s] : s;
+  const int32_t *m = rec_map<V>(B);
+  return m ? (int64_t)m[s] : s;
 }
 // feat_c row of policy row r = (env, slot, ped): with one pedestrian and the compact layout, feat_c
 // is the step's record obs_c[t] and row r its segment's record (-1: none)
+template <int V>
 __device__ __forceinline__ int64_t feat_row(const mhppo_rollout_bufs &B, int P, int64_t r) {
-  return P == 1 ? rec_index(B, r) : r;
+  return P == 1 ? rec_index<V>(B, r) : r;
 }
 
 template <int V>
@@ -140,7 +149,7 @@ __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp m
   const float *o = B.obs + e * L.obs_dim;
   float f[NF_C];
   float ex = obs_car_ped(o, L, i, p, f);
-  const int64_t fr = feat_row(B, c.P, (int64_t)r);
+  const int64_t fr = feat_row<V>(B, c.P, (int64_t)r);
   if (fr >= 0) {
     float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
@@ -193,7 +202,7 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
   const float *o = B.obs + (size_t)e * L.obs_dim;
   float f[NF_C];
   float ex = obs_car_ped(o, L, i, p, f);
-  const int64_t fr = feat_row(B, c.P, r);
+  const int64_t fr = feat_row<V>(B, c.P, r);
   if (fr >= 0) {
     float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
@@ -426,7 +435,7 @@ __global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__rest
     r_nxt = r_2;
     ok_nxt = ok_2;
     raw_cur = raw_nxt;
-    const int64_t fr = valid ? feat_row(B, c.P, r) : -1;
+    const int64_t fr = valid ? feat_row<V>(B, c.P, r) : -1;
     if (fr >= 0 && kh == 0) {
       float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
@@ -594,23 +603,24 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   // compile-time S multiple of 4: the step's act/logp/rew/ep_min records go out as vectors (the
   // identity record layout; the compact one stores each present segment's record at its index)
   constexpr bool REC_VEC = EV::CNS > 0 && EV::CNS % 4 == 0;
-  const bool vec = REC_VEC && !B.rec_of;
   // the compact layout on a full wave of the register-view step: records staged per wave (RecStage)
   constexpr bool STAGE = V == V_SCALABLE && REC_VEC && !REG_OUT;
+  const int32_t *rec_of = rec_map<V>(B);
+  const bool vec = REC_VEC && !rec_of;
   const int lane = threadIdx.x & 63;
   const int e0 = __builtin_amdgcn_readfirstlane(e - lane);
-  const bool staged = STAGE && B.rec_of && e0 + 64 <= c.N;
+  const bool staged = STAGE && rec_of && e0 + 64 <= c.N;
   int R0 = 0, K = 0;
   if (staged) {  // the wave's record run (uniform loads, issued with the other inputs)
-    R0 = B.rec_of[(size_t)c.N * S + e0];
-    K = B.rec_of[(size_t)c.N * S + e0 + 64] - R0;
+    R0 = rec_of[(size_t)c.N * S + e0];
+    K = rec_of[(size_t)c.N * S + e0 + 64] - R0;
   }
   // this env's records: its present slots (exist, set by mhppo_rollout_begin) in slot order from
   // the env's first record (one prefix load and the S exist bytes, not S rank loads)
   int64_t rbase = 0;
   uint32_t emask = 0;
-  if (B.rec_of) {
-    rbase = B.rec_of[(size_t)c.N * S + e];
+  if (rec_of) {
+    rbase = rec_of[(size_t)c.N * S + e];
     MHPPO_UNROLL
     for (int i = 0; i < S; i++) emask |= (uint32_t)(B.exist[(size_t)e * S + i] != 0) << i;
   }
@@ -636,7 +646,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
     if (loc != loc && B.status) atomicOr(B.status, 2u);  // MultivariateNormal raises on a NaN loc
     float z = eps[(size_t)e * S + i];
     float a = loc + MVN_L * z;
-    rix[i] = !B.rec_of ? (int64_t)e * S + i
+    rix[i] = !rec_of ? (int64_t)e * S + i
                        : (((emask >> i) & 1u) ? rbase + __builtin_popcount(emask & ((1u << i) - 1u)) : -1);
     const int64_t bt = (int64_t)t * c.N * S + rix[i];  // time-major records [T][N S]
     if (REC_VEC && (vec || staged)) {
@@ -840,7 +850,7 @@ __global__ void __launch_bounds__(TPB)
     float f[NF_C + 1];
     const float ex = obs_car_ped_raw(raw_cur, f);
     f[NF_C] = 0.0f;
-    const int64_t fr = ok_cur ? feat_row(B, 1, r_cur) : -1;  // (the fused step: one pedestrian)
+    const int64_t fr = ok_cur ? feat_row<V>(B, 1, r_cur) : -1;  // (the fused step: one pedestrian)
     if (fr >= 0 && kh == 0) {
       float *fo = B.feat_c + fr * NF_C;
 #pragma unroll
@@ -1432,6 +1442,7 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
   VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, *actor_choice, u, forced_a, *bufs);
   size_t NS = (size_t)c.N * c.nS;
   if (bufs->rec_of) {  // the compact record layout: present segments ranked in (env, slot) order
+    if (c.variant != V_SCALABLE) return set_error(MHPPO_EINVAL, "rec_of: the scalable env's layout only");
     if (!bufs->exist) return set_error(MHPPO_EINVAL, "rec_of needs exist");
     const int nblk = (int)grid_for(NS).x;
     int32_t *cnt = reinterpret_cast<int32_t *>(scratch((nblk + 1) / 2));
