@@ -754,6 +754,14 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 // of the same image.  Weight gradients sum over the tile's 32 rows: both operands go
 // through one per-wave bf16 image [row][feature] of the split parts, read back transposed.
 // Bias gradients and dW4 are f32 row sums through the same LDS slot.
+#ifndef MHPPO_X3_FLOSS
+// the continuous actor's ratio / clipped surrogate / dmu in float32 instead of the reference's
+// float64 ratio (A/B builds override); the float64 math's temporaries are what kept W3's forward
+// fragments out of the actor's registers
+#define MHPPO_X3_FLOSS 0
+#endif
+constexpr bool X3_FLOSS = MHPPO_X3_FLOSS;
+
 namespace x3 {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -1501,11 +1509,20 @@ struct Pass {
         const float diff = (float)((double)slot[G::IN_S1 + j] - (double)mu);
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-        const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
-        double dfdr;
-        const double f = surr_and_grad(r, (double)A, dfdr);
-        if (kh == 0) dsum0 += f;
-        const float dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+        float dmu;
+        if constexpr (X3_FLOSS) {  // the ratio and surrogate in float32 (MHPPO_X3_FLOSS)
+          const float r = expf(lp - slot[G::IN_S1 + 32 + j]);
+          float dfdr;
+          const float f = surr_and_grad_f(r, A, dfdr);
+          if (kh == 0) dsum0 += (double)f;
+          dmu = (float)inv_m * dfdr * r * x * MVN_INV_L;
+        } else {
+          const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
+          double dfdr;
+          const double f = surr_and_grad(r, (double)A, dfdr);
+          if (kh == 0) dsum0 += f;
+          dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
+        }
         dy0 = (dmu * out_std) * (1.0f - t * t);
       } else {
         // choice actor (train_model_d :818-851): softmax over the pair (as torch: shift by the

@@ -296,6 +296,21 @@ MHPPO_HD inline double surr_and_grad(double r, double A, double &dfdr) {
   dfdr = -g;
   return -(s1 < s2 ? s1 : s2);
 }
+// the same in float32 (the split-precision train kernel's continuous actor, MHPPO_X3_FLOSS)
+MHPPO_HD inline float surr_and_grad_f(float r, float A, float &dfdr) {
+  const float rc = r < 0.8f ? 0.8f : (r > 1.2f ? 1.2f : r);
+  const float s1 = r * A, s2 = rc * A;
+  const float in = (r >= 0.8f && r <= 1.2f) ? 1.0f : 0.0f;
+  float g;
+  if (s1 < s2)
+    g = A;
+  else if (s2 < s1)
+    g = in * A;
+  else
+    g = 0.5f * A + 0.5f * in * A;
+  dfdr = -g;
+  return -(s1 < s2 ? s1 : s2);
+}
 
 constexpr float MVN_INV_L = 0x1.6a09e6p+0f;    // float32(1/L) as torch's triangular solve uses
 constexpr float MVN_LOG2PI = 0x1.d67f1cp+0f;   // float32(1 * math.log(2*math.pi))

@@ -21,6 +21,9 @@ ap.add_argument("--choice-rows", type=int, default=655360)
 ap.add_argument("--sweep", action="store_true",
                 help="per-launch time of critic / actor passes at 1, 2, 4 ... 64 tiles per wave (kernel only, "
                      "HIP events around the x3 launch are not separable: reported per k_mlp_train call)")
+ap.add_argument("--data", default="randn", choices=("randn", "zero", "coarse"),
+                help="the observation rows: N(0, 9) (default), all zero, or N(0, 9) rounded to integers "
+                     "(MFMA timing does not depend on the data; a change here is the chip's power / clock state)")
 a = ap.parse_args()
 if a.sweep:
     torch.manual_seed(0)
@@ -53,6 +56,10 @@ torch.manual_seed(0)
 actor = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
 critic = Model_PPO(13, 1, 0).cuda()
 obs = torch.randn(M, 13, device="cuda") * 3
+if a.data == "zero":
+    obs.zero_()
+elif a.data == "coarse":
+    obs.round_()
 ret = torch.randn(M, device="cuda") * 8 - 20
 act = torch.randn(M, device="cuda") - 1
 lp = torch.randn(M, device="cuda") * 0.3 - 0.9
