@@ -228,6 +228,9 @@ __host__ __device__ __attribute__((noinline)) inline void mt_twist_into(const ui
   dst[623] = dst[396] ^ mt_mix(src[623], dst[0]);
 }
 
+#ifndef MHPPO_RNG_MULTI
+#define MHPPO_RNG_MULTI 1  // RngT::genrand_n's one-shift window path (A/B builds override)
+#endif
 // K > 0: the next K words of the active block are read ahead in one batch (independent
 // loads) and consumed in order; an empty window is refilled with one batch, so a run
 // of draws costs one HBM round trip per K words.
@@ -274,15 +277,39 @@ struct RngT {
       y = mt[mti];
     }
     mti++;
+    return temper(y);
+  }
+  MHPPO_HD static uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
   }
+  // the next n words (= n genrand() calls): with a window, one shift of it by n (n genrand()s shift
+  // it n times by one, ~K moves each); a run that crosses the active block's end takes genrand()
+  template <int n>
+  MHPPO_HD void genrand_n(uint32_t (&y)[n]) {
+    if (!MHPPO_RNG_MULTI || K < n || mti + n > MT_N) {
+#pragma unroll
+      for (int k = 0; k < n; k++) y[k] = genrand();
+      return;
+    }
+    if (nwin < n) prefetch();  // then nwin = min(MT_N - mti, K) >= n
+#pragma unroll
+    for (int k = 0; k < n; k++) y[k] = temper(win[k]);
+#pragma unroll
+    for (int k = 0; k + n < (K > 0 ? K : 1); k++) win[k] = win[k + n];
+    nwin -= n;
+    mti += n;
+  }
+  MHPPO_HD static double random53(uint32_t a, uint32_t b) {  // CPython random() of two words
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+  }
   MHPPO_HD double random() {
-    uint32_t a = genrand() >> 5, b = genrand() >> 6;
-    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+    uint32_t w[2];
+    genrand_n<2>(w);
+    return random53(w[0], w[1]);
   }
   MHPPO_HD uint32_t randbelow(uint32_t n) {
     if (!n) return 0;
@@ -297,8 +324,10 @@ struct RngT {
   MHPPO_HD double normalvariate(double mu, double sigma) {
     double z;
     for (;;) {
-      double u1 = random();
-      double u2 = 1.0 - random();
+      uint32_t w[4];  // the round's two random() calls, in order
+      genrand_n<4>(w);
+      double u1 = random53(w[0], w[1]);
+      double u2 = 1.0 - random53(w[2], w[3]);
       z = NV_MAGICCONST * (u1 - 0.5) / u2;
       double zz = z * z / 4.0;
       // Squeeze around CPython's test zz <= -log(u2) (same decisions, same draws): with

@@ -38,3 +38,21 @@ def test_clean_rollout_has_no_nan_flag():
     algo = _algo()
     algo.rollout.iterations_rand(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice)
     assert int(algo.rollout.gpu.status.item()) == 0
+
+
+def test_compact_records_rejected_for_a_fixed_slot_env():
+    """include/mhppo.h mhppo_rollout_bufs.rec_of: the scalable env's layout only (the kernels of the
+    other variants are compiled without it), so mhppo_rollout_begin refuses it elsewhere."""
+    import ctypes
+    from mhppo._lib import MhppoError
+    algo = _algo()
+    g = algo.rollout.gpu
+    N, S = g.a_d.shape[0], g.a_d.shape[1]
+    buf = torch.zeros(N * S + N + 1, dtype=torch.int32, device=g.a_d.device)
+    g._bufs.rec_of = ctypes.c_void_p(buf.data_ptr())
+    try:
+        with pytest.raises(MhppoError, match="scalable"):
+            algo.rollout.iterations_rand(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice)
+    finally:
+        g._bufs.rec_of = None
+    algo.rollout.iterations_rand(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice)
