@@ -322,26 +322,28 @@ struct RngT {
   MHPPO_HD int randint(int a, int b) { return a + (int)randbelow((uint32_t)(b - a + 1)); }
   MHPPO_HD double uniform(double a, double b) { return a + (b - a) * random(); }
   MHPPO_HD double normalvariate(double mu, double sigma) {
-    double z;
+    double t, u2;
     for (;;) {
       uint32_t w[4];  // the round's two random() calls, in order
       genrand_n<4>(w);
-      double u1 = random53(w[0], w[1]);
-      double u2 = 1.0 - random53(w[2], w[3]);
-      z = NV_MAGICCONST * (u1 - 0.5) / u2;
-      double zz = z * z / 4.0;
-      // Squeeze around CPython's test zz <= -log(u2) (same decisions, same draws): with
-      // r = 1 - u2 (exact: the second random()), r < -log(u2) < r / u2, and for r >= 2^-40
-      // both gaps are >= r^2 / 2, i.e. >= 2^-41 relative — far beyond the roundings of r / u2
-      // and of log — so zz <= r accepts and zz > r / u2 rejects without the log.
+      const double u1 = random53(w[0], w[1]);
+      u2 = 1.0 - random53(w[2], w[3]);
+      t = NV_MAGICCONST * (u1 - 0.5);  // CPython: z = t / u2, zz = z * z / 4, accept iff zz <= -log(u2)
+      // Squeeze around that test (same decisions, same draws): with r = 1 - u2 (exact: the second
+      // random()), r < -log(u2) < r / u2, and for r >= 2^-40 both gaps are >= r^2 / 2, i.e.
+      // >= 2^-41 relative.  zz is t^2 / (4 u2^2) within a few ulps, so q = t^2 / 4 against r u2^2
+      // and r u2 with a 2^-40 relative margin decides zz <= r (accept) and zz > r / u2 (reject)
+      // without a division; only a draw inside a margin (or r < 2^-40) takes the exact test.
       const double r = 1.0 - u2;
       if (r >= 0x1p-40) {
-        if (zz <= r) break;
-        if (zz > r / u2) continue;
+        const double q = t * t * 0.25, ru = r * u2;
+        if (q <= ru * u2 * (1.0 - 0x1p-40)) break;
+        if (q > ru * (1.0 + 0x1p-40)) continue;
       }
-      if (zz <= -log(u2)) break;
+      const double z = t / u2;
+      if (z * z / 4.0 <= -log(u2)) break;
     }
-    return mu + z * sigma;
+    return mu + (t / u2) * sigma;
   }
 };
 using Rng = RngT<0>;
