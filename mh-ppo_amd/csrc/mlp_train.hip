@@ -756,9 +756,15 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 // Bias gradients and dW4 are f32 row sums through the same LDS slot.
 #ifndef MHPPO_X3_FLOSS
 // the continuous actor's ratio / clipped surrogate / dmu in float32 instead of the reference's
-// float64 ratio (A/B builds override); the float64 math's temporaries are what kept W3's forward
-// fragments out of the actor's registers
-#define MHPPO_X3_FLOSS 0
+// float64 ratio (A/B builds override).  The float64 exp's temporaries are what kept W3's forward
+// fragments out of the actor's registers (MHPPO_X3_ACT 63 fits at 512 VGPRs with it): cfg3
+// iteration -1.4 % over three interleaved bench pairs (profiles/r05_floss/).  Numerics: lp and
+// logp_old are float32 within a factor 2 of each other, so lp - logp_old is exact in float32 and
+// expf adds ~1 ulp to r, i.e. ~1e-7 relative on dmu — the level of the difference mu itself has
+// from the reference's CPU GEMM.  dmu's product stays float64 with one rounding: a
+// float32 chain of four roundings there moved the 2-rank vs 1-rank nets of tests/test_dp_gpu.py
+// from <= 7.6e-7 to 6.4e-5 (tools/dp_diff.py).  The exact f32 kernel keeps the float64 ratio.
+#define MHPPO_X3_FLOSS 1
 #endif
 constexpr bool X3_FLOSS = MHPPO_X3_FLOSS;
 
@@ -1515,7 +1521,7 @@ struct Pass {
           float dfdr;
           const float f = surr_and_grad_f(r, A, dfdr);
           if (kh == 0) dsum0 += (double)f;
-          dmu = (float)inv_m * dfdr * r * x * MVN_INV_L;
+          dmu = (float)(inv_m * (double)dfdr * (double)r * (double)x * (double)MVN_INV_L);
         } else {
           const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
           double dfdr;
@@ -2400,8 +2406,10 @@ constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
 // the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
 // fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE (A/B overrides)
 // 61: both backward fragments held, dW4 in registers, DH2F + XCE, W2's forward fragments held (485
-// VGPRs since the forward writes the h images; -1.5 % vs 60, profiles/r05_x3/ab.txt; W3's too spill)
-#define MHPPO_X3_ACT 61
+// VGPRs since the forward writes the h images; -1.5 % vs 60, profiles/r05_x3/ab.txt); 63: W3's
+// forward fragments too, which fit (512 VGPRs, no spill) only with the float32 loss math
+// (MHPPO_X3_FLOSS; with the float64 ratio 63 spills 60 B)
+#define MHPPO_X3_ACT (MHPPO_X3_FLOSS ? 63 : 61)
 #endif
 constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
 constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
