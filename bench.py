@@ -84,22 +84,23 @@ def pmc_traffic(*patterns):
     separate FETCH_SIZE / WRITE_SIZE passes of this bench; reads = 2 x FETCH_SIZE on
     gfx950).  None when absent."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_cfg{CONFIG}.json")
-    try:
-        ks = json.load(open(path))["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
+    if not os.path.exists(path):
+        return None  # no PMC summary committed for this config: reported as null
+    ks = json.load(open(path))["kernels"]
     # a pattern is a substring or a tuple of substrings that must all occur in the kernel's name
     match = lambda k, p: all(q in k for q in p) if isinstance(p, tuple) else p in k  # noqa: E731
     vals = [v["hbm_bytes_per_launch"] for k, v in ks.items()
             if any(match(k, p) for p in patterns) and v.get("hbm_bytes_per_launch")]
-    return sum(vals) / len(vals) if vals else None
+    if not vals:  # a stale summary (kernel renamed since it was taken) must not pass as "no data"
+        raise RuntimeError(f"{path}: no PMC entry matches {patterns}; re-take it (tools/gpu_pmc.sh)")
+    return sum(vals) / len(vals)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
                     help="BASELINE.json config: 3 = 4cars 4/1/2 (the metric), 4 = scalable 8/1/4, 2 = coop 2/1/2")
     ap.add_argument("--envs", type=int, default=None,
@@ -208,9 +209,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-iteration GPU times (events on the current stream at the iteration boundaries: no extra
+    # synchronisation inside the timed region), so clock / power drift over the run is visible
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for k in range(a.steps):
         iteration()
+        marks[k + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -220,6 +226,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     ms = dt / a.steps * 1e3
+    iter_ms = [round(marks[k].elapsed_time(marks[k + 1]), 3) for k in range(a.steps)]
     value = world * N * T / (dt / a.steps)
     # After the timed region (same process, same workload): (0) one more training iteration with the
     # train passes on ONE stream and torch events around each launch -> roofline (the product runs
@@ -236,19 +243,18 @@ def main():
     ppo.TRAIN_STREAMS = streams_product
     gpu = algo.rollout.gpu
     env_ms, env_n = ctypes.c_double(0.0), ctypes.c_int32(0)
-    step_us, fused_kern_us = {}, None
-    modes = [("one_chain", 1, False)] + ([("parts", gpu.parts, False)] if gpu.parts > 1 else []) + \
-        ([("fused", 1, True)] if gpu.fused_ok else []) + [("product", None, None)]
+    step_us = {}
+    modes = [("one_chain", 1)] + ([("parts", gpu.parts)] if gpu.parts > 1 else []) + [("product", None)]
     with torch.no_grad():
-        for name, parts, fused in modes:
+        for name, parts in modes:
             algo.rollout.reset()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            timed = name in ("one_chain", "fused")
+            timed = name == "one_chain"
             if timed:
                 _lib.check(L.mhppo_kernel_timing_begin(T))
             e0.record()
             gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=7, iteration=0,
-                        parts=parts, fused=fused, graph=None if name == "product" else False)
+                        parts=parts, graph=None if name == "product" else False)
             e1.record()
             torch.cuda.synchronize()
             if timed:
@@ -256,10 +262,7 @@ def main():
                 _lib.check(L.mhppo_kernel_timing_end(ctypes.byref(ms_), ctypes.byref(n_)))
                 if n_.value != T:
                     raise RuntimeError(f"timed {n_.value} step launches, expected {T}")
-                if fused:
-                    fused_kern_us = ms_.value / T * 1e3
-                else:
-                    env_ms, env_n = ms_, n_
+                env_ms, env_n = ms_, n_
             step_us[name] = e0.elapsed_time(e1) * 1e3 / T
     kern_ms = env_ms.value / env_n.value
     S = venv.n_slots
@@ -275,7 +278,7 @@ def main():
     tr_tflops = tr_flops / (tr_ms * 1e-3) / 1e12
     split = not algo.exact_f32
     peak = X3_MFMA_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
-    traffic = (pmc_traffic(("k_mlp_train_x3<0", "Geo<16, 1, 13>"), ("k_mlp_train_x3<1", "Geo<16, 1, 13>")) if split else
+    traffic = (pmc_traffic(("k_mlp_train_x3<0", "Geo<16, 1, 13"), ("k_mlp_train_x3<1", "Geo<16, 1, 13")) if split else
                pmc_traffic("k_mlp_train<0, 7, true>", "k_mlp_train<1, 7, true>"))
     traffic_env = pmc_traffic("k_sample_env")
     agents = "ragged 1-8 existing of 8 slots" if variant == "scalable" else S
@@ -309,15 +312,14 @@ def main():
                          "bytes_per_launch": per_env * N, "bytes_per_env_step": per_env,
                          "kernel_ms": kern_ms, "step_kernel_env_steps_per_s": N / (kern_ms * 1e-3),
                          "measured_on": "one extra 80-step rollout after the timed region, all N envs per launch"},
-        "rollout_step_us": {**step_us, "parts_n": gpu.parts, "fused_kernel": fused_kern_us,
-                            "product_path": ("fused" if gpu.fused else ("parts" if gpu.parts > 1 else "one_chain")) +
-                            (" (HIP graph)" if gpu.use_graph and (gpu.parts == 1 or gpu.fused or gpu.use_graph == 2)
-                             else ""),
+        "rollout_step_us": {**step_us, "parts_n": gpu.parts,
+                            "product_path": ("parts" if gpu.parts > 1 else "one_chain") +
+                            (" (HIP graph)" if gpu.use_graph and (gpu.parts == 1 or gpu.use_graph == 2) else ""),
                             "note": "wall time per rollout step, torch events around a whole 80-step collect: "
                                     "one_chain = policy + env-step launches, parts = those on two streams "
-                                    "(env halves), fused = one launch per step (mhppo_rollout_step_fused; "
-                                    "fused_kernel = its dispatch-attached kernel time), product = the "
-                                    "product's collect (its step loop replays a captured HIP graph)"},
+                                    "(env halves), product = the product's collect (its step loop replays a "
+                                    "captured HIP graph at small N)"},
+        "iter_ms": iter_ms,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(a, variant, nc, npd, nl)

@@ -139,9 +139,9 @@ typedef struct mhppo_mlp {
  * of (env, slot) segments over t, see mhppo/rollout.py bucket_segments.
  * With P == 1, feat_c may point at obs_c + t*N*S*13 for step t (the selected feature row is
  * the only row, so the policy writes the record in place and sample_env copies nothing).
- * rows (optional, int32 [N*S*P + 2]): scratch for the head-sorted policy step — begin lists
- * the (env, slot, ped) rows of the cross head, then those of the wait head, counts last;
- * NULL selects the unsorted policy kernel (both are bit-identical). */
+ * rows (int32 [N*S*P + 2]; required by the policy step, which returns MHPPO_EINVAL without it):
+ * scratch for the head-sorted policy step — begin lists the (env, slot, ped) rows of the cross
+ * head, then those of the wait head, counts last. */
 typedef struct mhppo_rollout_bufs {
     float *feat_d, *probs_d, *logp_d;
     int32_t *a_d, *closest;
@@ -172,8 +172,9 @@ typedef struct mhppo_rollout_bufs {
                            The scalable env only (the variant whose car slots can be absent):
                            mhppo_rollout_begin returns MHPPO_EINVAL for another. */
 } mhppo_rollout_bufs;
-/* mhppo_rollout_bufs.flags: run the head-sorted policy step on the VALU kernel (SGPR weights)
- * instead of the MFMA kernel; both are bit-identical (A/B and tests) */
+/* mhppo_rollout_bufs.flags: run the policy step on the VALU reference kernels instead of the MFMA
+ * kernel (bit-identical).  Those kernels are compiled into the test build only
+ * (tests/lib/libmhppo_test.so, -DMHPPO_TEST_KERNELS); the shipped library returns MHPPO_EINVAL. */
 #define MHPPO_ROLLOUT_VALU_POLICY 1
 
 int mhppo_choice_dim(const mhppo_env *env);
@@ -227,16 +228,6 @@ int mhppo_rollout_policy_part(mhppo_env *env, const mhppo_mlp *actor_cross, cons
                               mhppo_rollout_bufs *bufs, int part, void *stream);
 int mhppo_rollout_sample_env_part(mhppo_env *env, const float *eps, int t, mhppo_rollout_bufs *bufs, int part,
                                   void *stream);
-
-/* Step t as ONE launch (one pedestrian per env, a compiled register-view shape: configs 2, 3
- * and 4): each wave runs the cross / wait actors for its envs' rows on f32 MFMA (the rows
- * compacted by head per wave) and then the sample / env step with the outputs in registers.
- * Results are bit-identical to mhppo_rollout_policy + mhppo_rollout_sample_env; feat_c must
- * point at obs_c + t*N*S*13; rows and parts are not used.  mhppo_rollout_fused_supported
- * returns 1 when the env's shape has the kernel, else 0 (then this returns MHPPO_EINVAL). */
-int mhppo_rollout_fused_supported(const mhppo_env *env);
-int mhppo_rollout_step_fused(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
-                             const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream);
 
 /* Measurement (bench.py): the next `n` env-step launches (mhppo_rollout_sample_env) of the
  * calling thread on the device current at this call carry HIP events attached to their dispatch

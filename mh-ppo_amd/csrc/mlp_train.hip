@@ -755,15 +755,18 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 // through one per-wave bf16 image [row][feature] of the split parts, read back transposed.
 // Bias gradients and dW4 are f32 row sums through the same LDS slot.
 #ifndef MHPPO_X3_FLOSS
-// the continuous actor's ratio / clipped surrogate / dmu in float32 instead of the reference's
-// float64 ratio (A/B builds override).  The float64 exp's temporaries are what kept W3's forward
-// fragments out of the actor's registers (MHPPO_X3_ACT 63 fits at 512 VGPRs with it): cfg3
-// iteration -1.4 % over three interleaved bench pairs (profiles/r05_floss/).  Numerics: lp and
-// logp_old are float32 within a factor 2 of each other, so lp - logp_old is exact in float32 and
-// expf adds ~1 ulp to r, i.e. ~1e-7 relative on dmu — the level of the difference mu itself has
-// from the reference's CPU GEMM.  dmu's product stays float64 with one rounding: a
-// float32 chain of four roundings there moved the 2-rank vs 1-rank nets of tests/test_dp_gpu.py
-// from <= 7.6e-7 to 6.4e-5 (tools/dp_diff.py).  The exact f32 kernel keeps the float64 ratio.
+// the continuous actor's ratio magnitude r = expf(lp - logp_old) in float32, its clip branch
+// decided on the float64 difference lp - logp_old (surr_and_grad_fd: the reference's float64
+// ratio's decision, Coop-MH-PPO-scalable.py:803-806), instead of a float64 exp (A/B builds
+// override).  The float64 exp's temporaries are what kept W3's forward fragments out of the
+// actor's registers (MHPPO_X3_ACT 63 fits at 512 VGPRs without them): cfg3 iteration -1.4 % over
+// three interleaved bench pairs (profiles/r05_floss/).  Numerics: lp - logp_old in float32 is
+// exact only while the two are within a factor 2 of each other (Sterbenz), which updates do not
+// guarantee row by row, so r carries up to two float32 roundings (~1.2e-7 relative) — the level
+// of the difference mu itself has from the reference's CPU GEMM; the clip decision carries none
+// (DESIGN.md §5).  dmu's product stays float64 with one rounding: a float32 chain of four
+// roundings there moved the 2-rank vs 1-rank nets of tests/test_dp_gpu.py from <= 7.6e-7 to
+// 6.4e-5 (tools/dp_diff.py).  The exact f32 kernel keeps the float64 ratio.
 #define MHPPO_X3_FLOSS 1
 #endif
 constexpr bool X3_FLOSS = MHPPO_X3_FLOSS;
@@ -1516,10 +1519,11 @@ struct Pass {
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
         float dmu;
-        if constexpr (X3_FLOSS) {  // the ratio and surrogate in float32 (MHPPO_X3_FLOSS)
-          const float r = expf(lp - slot[G::IN_S1 + 32 + j]);
+        if constexpr (X3_FLOSS) {  // the ratio in float32, its clip branch decided in float64
+          const float lpo = slot[G::IN_S1 + 32 + j];
+          const float r = expf(lp - lpo);
           float dfdr;
-          const float f = surr_and_grad_f(r, A, dfdr);
+          const float f = surr_and_grad_fd(r, (double)lp - (double)lpo, A, dfdr);
           if (kh == 0) dsum0 += (double)f;
           dmu = (float)(inv_m * (double)dfdr * (double)r * (double)x * (double)MVN_INV_L);
         } else {
@@ -2445,6 +2449,11 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   prefetch_first<KIND, G>(ws, gw, M, X, nin, ret, V, act, lp_old);
   stage_net<G>(W, L8, tid, nin);
   __syncthreads();
+#ifdef MHPPO_X3_STAGGER
+  // A/B builds only: wave w of the block starts w x MHPPO_X3_STAGGER x 64 cycles late, so the
+  // four waves of a CU reach their LDS-store blocks and input DMA out of phase
+  for (int i = 0; i < w; i++) __builtin_amdgcn_s_sleep(MHPPO_X3_STAGGER);
+#endif
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
   constexpr bool C13 = KIND == K_CRITIC && G::NIC == NIN_CONT;  // the 13-input critic

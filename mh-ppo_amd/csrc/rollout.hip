@@ -3,8 +3,8 @@
 // Per PPO iteration (Env_rollout.iterations_rand + Algo_PPO.train,
 // Coop-MH-PPO-scalable.py:357-517, :658-684, :778-917), for N envs at once:
 //   begin:  env reset -> choice features -> choice actor -> Categorical draw
-//   step t: [k_policy] one lane per (env, slot, ped): obs_car_ped features and
-//           the cross/wait actor picked by action_d, weights staged in LDS;
+//   step t: [k_policy_mfma] per (env, slot, ped) row: obs_car_ped features and the
+//           cross/wait actor picked by action_d (head-sorted 32-row f32-MFMA tiles);
 //           [k_sample_env] one lane per env: min over pedestrians, MVN draw,
 //           log-prob, rollout-buffer writes, then the env step itself (the same
 //           env_step_one the standalone step kernel runs) and the episodic min.
@@ -131,6 +131,9 @@ __device__ __forceinline__ int64_t feat_row(const mhppo_rollout_bufs &B, int P, 
   return P == 1 ? rec_index<V>(B, r) : r;
 }
 
+#ifdef MHPPO_TEST_KERNELS
+// The VALU policy kernels (test build only, tests/lib/libmhppo_test.so: the bit-identity reference of
+// k_policy_mfma, tests/test_rollout_gpu.py).  The shipped library runs k_policy_mfma alone.
 template <int V>
 __global__ void __launch_bounds__(TPB) k_policy(Cfg c, mhppo_mlp mc, mhppo_mlp mw, mhppo_rollout_bufs B) {
   extern __shared__ float lds[];
@@ -214,6 +217,7 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
   const float t = mhppo_tanhf(out) * (head ? std_w : std_c);
   B.out_c[r] = t + (head ? mean_w : mean_c);
 }
+#endif  // MHPPO_TEST_KERNELS
 
 // ------------------------------------------------------- MFMA policy step
 // k_policy_mfma: the head-sorted rows as 32-row tiles on f32 MFMA (v_mfma_f32_32x32x2_f32, the
@@ -581,11 +585,9 @@ __device__ __forceinline__ RecStage<CNS> *rec_stage_wave() {
 // one lane per env: select/min over peds, MVN sample, buffers, env step, episodic min.
 // All of this lane's rollout inputs are read before any buffer write so the loads
 // issue as one batch; EV is the generic or the register env view.
-template <class EV, bool REG_OUT = false>
+template <class EV>
 __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__ eps, int t,
-                                                const mhppo_rollout_bufs &B, const float *outr = nullptr) {
-  // REG_OUT (the fused step, one pedestrian): slot i's actor output is outr[i], not out_c
-  static_assert(!REG_OUT || EV::CNP == 1, "register outputs: one pedestrian");
+                                                const mhppo_rollout_bufs &B) {
   constexpr int V = EV::VAR;
   const Cfg &c = E.c;
   const int e = E.e;
@@ -604,7 +606,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
   // identity record layout; the compact one stores each present segment's record at its index)
   constexpr bool REC_VEC = EV::CNS > 0 && EV::CNS % 4 == 0;
   // the compact layout on a full wave of the register-view step: records staged per wave (RecStage)
-  constexpr bool STAGE = V == V_SCALABLE && REC_VEC && !REG_OUT;
+  constexpr bool STAGE = V == V_SCALABLE && REC_VEC;
   const int32_t *rec_of = rec_map<V>(B);
   const bool vec = REC_VEC && !rec_of;
   const int lane = threadIdx.x & 63;
@@ -639,7 +641,7 @@ __device__ __forceinline__ void sample_env_body(EV &E, const float *__restrict__
       if constexpr (V == V_SCALABLE) {
         if (EV::CNP > 0 ? !(E.pflag(p) & F_EXIST) : o[L.ped_off + p * 9 + 7] == 0.0f) continue;
       }
-      float out = REG_OUT ? outr[i] : B.out_c[row0 + p];
+      float out = B.out_c[row0 + p];
       loc = t_minimum(loc, out);
       if (out == loc) sel = p;
     }
@@ -775,105 +777,6 @@ __global__ void __launch_bounds__(TPB)
     g_wave_times[2 * wv + 1] = wt1;
   }
 #endif
-}
-
-// -------------------------------------------------------------- fused step (one pedestrian)
-// The whole rollout step in one launch (Env_rollout.iterations_rand :430-461 policy forward, then
-// the sample / env.step of k_sample_env_r): each wave first runs the cross / wait actors for its
-// 64 envs' S rows — k_policy_mfma's 32-row f32-MFMA tiles (actor_tile: the same bits), the rows
-// compacted by head in LDS per wave (cross rows, then wait rows from the next 32-row boundary,
-// so each tile is one actor) — then sample_env_body on the register env view takes the outputs
-// from registers.  Saves the policy launch and its out_c round trip; the tile-0 gathers and the
-// env-state loads are issued before the first tile, so they land under the MFMA work.
-template <int V, int NC, int NAV, int NP>
-__global__ void __launch_bounds__(TPB)
-    k_step_fused(Cfg c, Bufs eb, const float *__restrict__ Wc, const float *__restrict__ Ww, float mean_c,
-                 float std_c, float mean_w, float std_w, const float *eps, int t, mhppo_rollout_bufs B, int e_lo,
-                 int e_hi) {
-  using namespace pol;
-  using EV = EnvR<V, NC, NAV, NP>;
-  constexpr int S = EV::CNS, ROWS = 64 * S + 32;
-  static_assert(NP == 1 && S > 0, "fused step: one pedestrian, compile-time slots");
-  extern __shared__ float lds[];  // [2][HEAD] actors | per wave: row list [ROWS] | outputs [ROWS]
-  const int tid = threadIdx.x, l = tid & 63, j = l & 31, kh = l >> 5, w = tid >> 6;
-  int *list = reinterpret_cast<int *>(lds + 2 * HEAD) + w * 2 * ROWS;
-  float *outs = reinterpret_cast<float *>(list + ROWS);
-  const int e = e_lo + blockIdx.x * TPB + tid;
-  const bool act = e < e_hi;
-  int ad[S];  // this lane's rows' choices (cross when 0: k_head_count), fixed for the episode
-#pragma unroll
-  for (int i = 0; i < S; i++) ad[i] = act ? B.a_d[(size_t)e * S + i] : 1;
-  stage_both<TPB>(lds, Wc, Ww, tid);
-  // per-wave compaction: cross rows at [0, nc), wait rows at [32 tc, 32 tc + nw)
-  const uint64_t below = l ? (~0ull >> (64 - l)) : 0ull;
-  int pos[S], nc = 0, nw = 0;
-#pragma unroll
-  for (int i = 0; i < S; i++) {
-    const uint64_t m = __ballot(act && ad[i] == 0);
-    pos[i] = nc + __popcll(m & below);
-    nc += __popcll(m);
-  }
-  const int tc = (nc + 31) / 32;
-#pragma unroll
-  for (int i = 0; i < S; i++) {
-    const uint64_t m = __ballot(act && ad[i] != 0);
-    if (ad[i] != 0) pos[i] = 32 * tc + nw + __popcll(m & below);
-    nw += __popcll(m);
-  }
-#pragma unroll
-  for (int i = 0; i < S; i++)
-    if (act) list[pos[i]] = e * S + i;  // the global row (env, slot), P = 1
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int ntiles = tc + (nw + 31) / 32, wend = 32 * tc + nw;
-  const ObsLayout L = obs_layout(c);
-  auto tile_raw = [&](int tl, int &r, bool &ok) {
-    const int p0 = 32 * tl + j;
-    ok = tl < tc ? p0 < nc : p0 < wend;
-    r = list[ok ? p0 : 32 * tl];  // an invalid lane gathers its tile's first (valid) row
-    const int ee = r / S;
-    return feat_raw(B.obs + (size_t)ee * L.obs_dim, L, r - ee * S, 0);
-  };
-  int r_cur = 0;
-  bool ok_cur = false;
-  FeatRaw raw_cur;
-  if (ntiles > 0) raw_cur = tile_raw(0, r_cur, ok_cur);
-  EV E(c, eb, act ? e : e_lo);  // the env-state loads, in flight under the tiles (a spare lane: a valid env)
-  __syncthreads();              // both actors staged
-  for (int tile = 0; tile < ntiles; tile++) {
-    int r_nxt = r_cur;
-    bool ok_nxt = false;
-    FeatRaw raw_nxt = raw_cur;
-    if (tile + 1 < ntiles) raw_nxt = tile_raw(tile + 1, r_nxt, ok_nxt);
-    const int head = tile >= tc;
-    float f[NF_C + 1];
-    const float ex = obs_car_ped_raw(raw_cur, f);
-    f[NF_C] = 0.0f;
-    const int64_t fr = ok_cur ? feat_row<V>(B, 1, r_cur) : -1;  // (the fused step: one pedestrian)
-    if (fr >= 0 && kh == 0) {
-      float *fo = B.feat_c + fr * NF_C;
-#pragma unroll
-      for (int q = 0; q < NF_C; q++) fo[q] = f[q];
-    }
-    const float out = actor_tile(lds + head * HEAD, f, j, kh);
-    if (ok_cur && kh == 0 && !(L.scalable && ex == 0.0f)) {  // `if exist:` gate (:439)
-      const float tv = mhppo_tanhf(out) * (head ? std_w : std_c) + (head ? mean_w : mean_c);
-      B.out_c[r_cur] = tv;
-      outs[32 * tile + j] = tv;
-    }
-    r_cur = r_nxt;
-    ok_cur = ok_nxt;
-    raw_cur = raw_nxt;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (!act) return;
-  float outr[S];
-#pragma unroll
-  for (int i = 0; i < S; i++) outr[i] = outs[pos[i]];  // a gated row's value is never read
-  sample_env_body<EV, true>(E, eps, t, B, outr);
 }
 
 // -------------------------------------------------------------- evaluation
@@ -1330,33 +1233,6 @@ bool launch_sample_reg(const Cfg &c, const Bufs &eb, const float *eps, int t, co
   }
 }
 
-// the fused step for a compiled one-pedestrian shape (false: no such kernel; 4cars2 has no driver)
-template <int V, int NC, int NAV, int NP>
-bool launch_step_fused(const Cfg &c, const Bufs &eb, const mhppo_mlp &mc, const mhppo_mlp &mw, const float *eps, int t,
-                       const mhppo_rollout_bufs &B, hipStream_t s) {
-  if constexpr (V == V_4CARS2 || NP != 1) {
-    return false;
-  } else {
-    if (!use_reg_view(c, V, NC, NAV, NP)) return false;
-    constexpr int ROWS = 64 * EnvR<V, NC, NAV, NP>::CNS + 32;
-    const size_t shm = sizeof(float) * (2 * pol::HEAD + (TPB / 64) * 2 * ROWS);
-    const dim3 g = grid_for((size_t)c.N);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (ktime_next(e0, e1))
-      hipExtLaunchKernelGGL((k_step_fused<V, NC, NAV, NP>), g, dim3(TPB), shm, s, e0, e1, 0, c, eb, mc.packed,
-                            mw.packed, mc.mean, mc.std, mw.mean, mw.std, eps, t, B, 0, c.N);
-    else
-      hipLaunchKernelGGL((k_step_fused<V, NC, NAV, NP>), g, dim3(TPB), shm, s, c, eb, mc.packed, mw.packed, mc.mean,
-                         mc.std, mw.mean, mw.std, eps, t, B, 0, c.N);
-    return true;
-  }
-}
-template <int V, int NC, int NAV, int NP>
-bool has_step_fused(const Cfg &c) {
-  if constexpr (V == V_4CARS2 || NP != 1) return false;
-  else return use_reg_view(c, V, NC, NAV, NP);
-}
-
 // Env range of part `part` of `nparts` (the two-stream rollout, RolloutGPU(parts=2)): boundaries at
 // multiples of 64 envs (whole waves), the last part ends at N
 __host__ __device__ inline int part_env(const Cfg &c, int part, int nparts) {
@@ -1451,7 +1327,7 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
     hipLaunchKernelGGL(k_flag_rank, grid_for(NS), dim3(TPB), 0, s, bufs->exist, (int)NS, cnt, nblk, bufs->rec_of,
                        c.nS, bufs->rec_of + NS);
   }
-  if (bufs->rows) {  // head lists for k_policy_sorted (the choice is fixed for the episode)
+  if (bufs->rows) {  // head lists for k_policy_mfma (the choice is fixed for the episode)
     const int nblk = (int)grid_for(R).x;
     int32_t *cnt = reinterpret_cast<int32_t *>(scratch(nblk));
     if (!cnt) return set_error(MHPPO_ENOMEM, "scratch allocation failed");
@@ -1495,7 +1371,8 @@ static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mh
   const Cfg &c = env_cfg(env);
   size_t R = (size_t)c.N * c.nS * c.P;
   if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
-  if (bufs->rows && !(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
+  if (!bufs->rows) return set_error(MHPPO_EINVAL, "the policy step needs the head lists (bufs->rows)");
+  if (!(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
     // persistent 32-row MFMA tiles: 2 blocks per CU
     static int cus[mhppo::MAX_DEVICES] = {0};
     const int dev = env_device(env);
@@ -1515,19 +1392,23 @@ static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mh
     CHECK_HIP(hipGetLastError());
     return MHPPO_OK;
   }
-  if (bufs->rows) {
-    // one wave per 64 rows of one head: at most R/64 + 2 waves
+#ifdef MHPPO_TEST_KERNELS
+  // the VALU reference: one wave per 64 rows of one head (at most R/64 + 2 waves), or with
+  // MHPPO_ROLLOUT_VALU_POLICY | 2 the unsorted one-lane-per-row kernel
+  if (bufs->flags & 2) {
+    size_t shm = 2 * sizeof(float) * mlp_size(NF_C, 1);
+    VLAUNCH(k_policy, c.variant, grid_for(R), shm, (hipStream_t)stream, c, *actor_cross, *actor_wait, *bufs);
+  } else {
     const size_t waves = (R + 63) / 64 + 2;
     const dim3 grid((unsigned)((waves + TPB / 64 - 1) / (TPB / 64)));
     VLAUNCH(k_policy_sorted, c.variant, grid, 0, (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed,
             actor_cross->mean, actor_cross->std, actor_wait->mean, actor_wait->std, *bufs, env_bufs(env));
-    CHECK_HIP(hipGetLastError());
-    return MHPPO_OK;
   }
-  size_t shm = 2 * sizeof(float) * mlp_size(NF_C, 1);
-  VLAUNCH(k_policy, c.variant, grid_for(R), shm, (hipStream_t)stream, c, *actor_cross, *actor_wait, *bufs);
   CHECK_HIP(hipGetLastError());
   return MHPPO_OK;
+#else
+  return set_error(MHPPO_EINVAL, "MHPPO_ROLLOUT_VALU_POLICY: the VALU policy kernels are in the test build only");
+#endif
 }
 
 int mhppo_kernel_timing_begin(int n) {
@@ -1586,6 +1467,10 @@ static int rollout_sample_env(mhppo_env *env, const float *eps, int t, mhppo_rol
   if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
   GUARD_DEVICE(env_device(env));
   const Cfg &c = env_cfg(env);
+  // the compact layout with one pedestrian: the policy wrote each row's features at its record index,
+  // which only the in-place record (feat_c = obs_c[t]) reads back at the right place
+  if (bufs->rec_of && c.P == 1 && bufs->feat_c != bufs->obs_c + (size_t)t * c.N * c.nS * NF_C)
+    return set_error(MHPPO_EINVAL, "rec_of with one pedestrian: feat_c must point at obs_c[t]");
   const int e_lo = part_env(c, part, nparts), e_hi = part_env(c, part + 1, nparts);
   if (e_hi <= e_lo) return MHPPO_OK;  // an empty part (N < 64 nparts)
 #define SAMPLE_REG(V_, NC_, NAV_, NP_)                                                                      \
@@ -1618,38 +1503,6 @@ int mhppo_rollout_step(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo
   int rc = mhppo_rollout_policy(env, actor_cross, actor_wait, bufs, stream);
   if (rc) return rc;
   return mhppo_rollout_sample_env(env, eps, t, bufs, stream);
-}
-
-int mhppo_rollout_fused_supported(const mhppo_env *env) {
-  if (!env) return set_error(MHPPO_EINVAL, "null argument");
-  const Cfg &c = env_cfg(env);
-#define HAS_FUSED(V_, NC_, NAV_, NP_) \
-  if (has_step_fused<V_, NC_, NAV_, NP_>(c)) return 1;
-  MHPPO_REG_SHAPES(HAS_FUSED)
-#undef HAS_FUSED
-  return 0;
-}
-
-int mhppo_rollout_step_fused(mhppo_env *env, const mhppo_mlp *actor_cross, const mhppo_mlp *actor_wait,
-                             const float *eps, int t, mhppo_rollout_bufs *bufs, void *stream) {
-  if (!env || !actor_cross || !actor_wait || !eps || !bufs) return set_error(MHPPO_EINVAL, "null argument");
-  if (actor_cross->n_in != NF_C || actor_wait->n_in != NF_C || actor_cross->n_out != 1 || actor_wait->n_out != 1)
-    return set_error(MHPPO_EINVAL, "continuous actors must be 13 -> 1");
-  if (t < 0 || t >= bufs->T) return set_error(MHPPO_EINVAL, "step %d outside [0, %d)", t, bufs->T);
-  GUARD_DEVICE(env_device(env));
-  const Cfg &c = env_cfg(env);
-  if ((size_t)c.N * c.nS * c.P > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
-  if (bufs->feat_c != bufs->obs_c + (size_t)t * c.N * c.nS * NF_C)
-    return set_error(MHPPO_EINVAL, "fused step: feat_c must point at obs_c[t]");
-#define STEP_FUSED(V_, NC_, NAV_, NP_)                                                                           \
-  if (launch_step_fused<V_, NC_, NAV_, NP_>(c, env_bufs(env), *actor_cross, *actor_wait, eps, t, *bufs,          \
-                                            (hipStream_t)stream)) {                                              \
-    CHECK_HIP(hipGetLastError());                                                                                \
-    return MHPPO_OK;                                                                                             \
-  }
-  MHPPO_REG_SHAPES(STEP_FUSED)
-#undef STEP_FUSED
-  return set_error(MHPPO_EINVAL, "no fused step kernel for this shape (mhppo_rollout_fused_supported)");
 }
 
 int mhppo_rollout_check(mhppo_rollout_bufs *bufs, void *stream) {

@@ -296,19 +296,23 @@ MHPPO_HD inline double surr_and_grad(double r, double A, double &dfdr) {
   dfdr = -g;
   return -(s1 < s2 ? s1 : s2);
 }
-// the same in float32 (the split-precision train kernel's continuous actor, MHPPO_X3_FLOSS)
-MHPPO_HD inline float surr_and_grad_f(float r, float A, float &dfdr) {
-  const float rc = r < 0.8f ? 0.8f : (r > 1.2f ? 1.2f : r);
+// The same with the ratio's magnitude in float32 and its clip branch decided in float64 (the
+// split-precision train kernel's continuous actor).  r = expf(lp - lp_old) carries ~2 float32
+// roundings; which branch the reference's float64 ratio takes depends only on
+// d = lp - lp_old in float64 (exact: a difference of two floats), against ln 0.8 / ln 1.2:
+//   A > 0: -min(rA, clamp(r)A) follows r up to r = 1.2 (dfdr = -A), then is constant;
+//   A < 0: it follows r from r = 0.8 on, and is constant below.
+// (At r in [0.8, 1.2] the two terms tie and torch's minimum splits the gradient evenly between
+// them, 0.5 A + 0.5 A.)  d is a multiple of 2^-24 for log-densities below -0.5, whose grid points lie
+// >= 8e-9 from ln 0.8 and ln 1.2, far outside a float64 rounding of them: the decision is the float64 ratio's
+// (tests/test_update_scale_gpu.py counts the rows a float32 decision would flip).
+constexpr double LN_0_8 = -0x1.c8ff7c79a9a20p-3, LN_1_2 = 0x1.7565011e49675p-3;  // float64 log(0.8), log(1.2)
+MHPPO_HD inline float surr_and_grad_fd(float r, double d, float A, float &dfdr) {
+  const bool lo = d < LN_0_8, hi = d > LN_1_2;  // r < 0.8, r > 1.2 in float64
+  const float rc = lo ? 0.8f : (hi ? 1.2f : r);
+  const bool follow = A > 0.0f ? !hi : (A < 0.0f && !lo);
+  dfdr = follow ? -A : 0.0f;
   const float s1 = r * A, s2 = rc * A;
-  const float in = (r >= 0.8f && r <= 1.2f) ? 1.0f : 0.0f;
-  float g;
-  if (s1 < s2)
-    g = A;
-  else if (s2 < s1)
-    g = in * A;
-  else
-    g = 0.5f * A + 0.5f * in * A;
-  dfdr = -g;
   return -(s1 < s2 ? s1 : s2);
 }
 

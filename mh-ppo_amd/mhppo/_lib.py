@@ -69,9 +69,6 @@ _SIGS = {
     "mhppo_rollout_begin": (I32, [P, ctypes.POINTER(Mlp), P, P, ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_step": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), P, I32,
                                  ctypes.POINTER(RolloutBufs), P]),
-    "mhppo_rollout_step_fused": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), P, I32,
-                                       ctypes.POINTER(RolloutBufs), P]),
-    "mhppo_rollout_fused_supported": (I32, [P]),
     "mhppo_rollout_policy": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_sample_env": (I32, [P, P, I32, ctypes.POINTER(RolloutBufs), P]),
     "mhppo_rollout_policy_part": (I32, [P, ctypes.POINTER(Mlp), ctypes.POINTER(Mlp), ctypes.POINTER(RolloutBufs), I32,

@@ -3,8 +3,8 @@
 Batched form of `Env_rollout.iterations_rand` (Coop-MH-PPO-scalable.py:357-517;
 coop driver Coop-MH-PPO.ipynb cell 0): every env plays one 80-step episode;
 the choice head is sampled once at t=0 (ped_traffic never changes, so
-`need_new_d` is only true at the start); each step runs the fused
-policy kernel and the fused sample+env-step kernel.  The per-step records are
+`need_new_d` is only true at the start); each step runs the
+MFMA policy kernel and the fused sample+env-step kernel.  The per-step records are
 written time-major, [t, env, slot] (each step's writes are one contiguous block
 in HBM); RolloutBatch exposes them as [env, slot, t] views, and bucket_segments
 gathers (env, slot) segments over t into the reference's episode-major,
@@ -30,7 +30,9 @@ class RolloutBatch:
     """Views of one iteration's rollout buffers (all on the env's device).  With the compact
     record layout (rec_of set: the scalable env, whose absent car slots store no records) obs_c /
     act / logp / rew are gathered from the time-major records on first access, absent segments
-    zero."""
+    zero — a full copy, not a view: at config 4 (524 288 segments x 80 steps) obs_c alone is
+    2.2 GB, and the gather needs about twice that in temporaries.  The product path never touches
+    them (bucket_segments reads the *_tm records through rec_of); they are for tests and tools."""
 
     _REC = ("obs_c", "act", "logp", "rew")
 
@@ -73,17 +75,8 @@ def default_graph():
     return {"0": 0, "2": 2}.get(os.environ.get("MHPPO_ROLLOUT_GRAPH", "1"), 1)
 
 
-def default_fused():
-    """Off unless MHPPO_ROLLOUT_FUSED=1: the one-launch step (mhppo_rollout_step_fused) is
-    bit-identical but measured slower than the two-stream parts (config 3: 71 us per fused launch
-    against 64 us per two-part step, profiles/r04_fused/): at one wave per SIMD (the env step's
-    315 registers) its actors' MFMA chains and the env step run back to back in each wave."""
-    import os
-    return os.environ.get("MHPPO_ROLLOUT_FUSED", "0") == "1"
-
-
 class RolloutGPU:
-    def __init__(self, venv, T=None, valu_policy=False, parts=None, fused=None):
+    def __init__(self, venv, T=None, valu_policy=False, parts=None):
         if venv.variant == "4cars2":
             raise ValueError("4cars2 is an env-level variant only: the reference has no driver for it and its "
                              "PPO-driven followers earn no reward (Env_hybrid_multi_coop_4cars2.py:836-847)")
@@ -118,9 +111,6 @@ class RolloutGPU:
         self.compact = venv.variant == "scalable" and os.environ.get("MHPPO_COMPACT_RECORDS", "1") != "0"
         self.rec_buf = z(N * S + N + 1, i32) if self.compact else None  # segment ranks | per-env prefix
         self.rec_of = self.rec_buf[:N * S] if self.compact else None
-        # the fused one-launch step (one pedestrian, compiled shapes): bit-identical to the two launches
-        self.fused_ok = bool(_lib.lib().mhppo_rollout_fused_supported(venv.handle) == 1) and not valu_policy
-        self.fused = self.fused_ok and (default_fused() if fused is None else bool(fused))
         self.parts = default_parts(N, valu_policy) if parts is None else int(parts)
         if self.parts > 1 and valu_policy:
             raise ValueError("parts > 1 runs the MFMA policy kernel only")
@@ -133,8 +123,10 @@ class RolloutGPU:
             setattr(b, name, ctypes.c_void_p(getattr(self, name).data_ptr()))
         b.T = self.T
         b.rec_of = ctypes.c_void_p(self.rec_buf.data_ptr()) if self.compact else None
-        # policy step on the VALU kernel instead of the MFMA one (bit-identical; A/B and tests)
-        b.flags = 1 if valu_policy else 0  # MHPPO_ROLLOUT_VALU_POLICY
+        # policy step on the VALU reference kernels instead of the MFMA one (bit-identical; tests, with
+        # the test build of the library: MHPPO_LIB=tests/lib/libmhppo_test.so); "unsorted": the
+        # one-lane-per-row kernel
+        b.flags = {False: 0, True: 1, "unsorted": 3}[valu_policy]  # MHPPO_ROLLOUT_VALU_POLICY
         b.parts = self.parts
         self._bufs = b
         # captured one-chain step loops, keyed by what their launches bake in (collect)
@@ -200,23 +192,17 @@ class RolloutGPU:
         _lib.check(L.mhppo_philox_normal_2d(key, _CTR_STEP + off * self.S, _CTR_STEP, _lib.ptr(self.eps), self.T,
                                             self.eps[0].numel(), st))
 
-    def _step_loop(self, L, mx, mw, fused, st, step_events):
-        """The T steps as one chain on stream `st`: the fused launch, or policy + env step."""
+    def _step_loop(self, L, mx, mw, st, step_events):
+        """The T steps as one chain on stream `st`: policy + env step."""
         for t in range(self.T):
             if self.P == 1:  # features straight into the step's record (include/mhppo.h)
                 self._bufs.feat_c = self.obs_c[t].data_ptr()
-            if fused:
-                if step_events is not None:
-                    step_events[t][0].record()
-                _lib.check(L.mhppo_rollout_step_fused(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
-                                                      _lib.ptr(self.eps[t]), t, ctypes.byref(self._bufs), st))
-            else:
-                _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+            _lib.check(L.mhppo_rollout_policy(self.venv.handle, ctypes.byref(mx), ctypes.byref(mw),
+                                              ctypes.byref(self._bufs), st))
+            if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
+                step_events[t][0].record()
+            _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
                                                   ctypes.byref(self._bufs), st))
-                if step_events is not None:  # HIP events bracketing the env-step kernel on this stream
-                    step_events[t][0].record()
-                _lib.check(L.mhppo_rollout_sample_env(self.venv.handle, _lib.ptr(self.eps[t]), t,
-                                                      ctypes.byref(self._bufs), st))
             if step_events is not None:
                 step_events[t][1].record()
 
@@ -243,18 +229,16 @@ class RolloutGPU:
             main.wait_stream(side)
 
     def collect(self, actor_cross, actor_wait, actor_choice, seed=0, iteration=0, forced_choice=None,
-                eps_tape=None, step_events=None, parts=None, fused=None, graph=None):
+                eps_tape=None, step_events=None, parts=None, graph=None):
         """Run one episode in every env.  forced_choice int32 [N,S,P] / eps_tape float32 [T,N,S]
-        replay recorded draws (parity mode); otherwise Philox noise is drawn.  fused: the one-launch
-        step (default: self.fused; needs self.fused_ok).  Unfused, parts: 1 forces the one-chain
-        loop for this call (default: self.parts); step_events implies it.  step_events brackets
-        each step's env-step launch (the fused launch when fused).  graph: replay the step loop
+        replay recorded draws (parity mode); otherwise Philox noise is drawn.  parts: 1 forces the
+        one-chain loop for this call (default: self.parts); step_events implies it.  step_events
+        brackets each step's env-step launch.  graph: replay the step loop
         from a captured HIP graph (default: self.use_graph; pass False while mhppo_kernel_timing is
         on — graph nodes carry no timing events)."""
         L = _lib.lib()
-        fused = self.fused if fused is None else (bool(fused) and self.fused_ok)
         nparts = self.parts if parts is None else min(int(parts), self.parts)
-        if step_events is not None or fused:
+        if step_events is not None:
             nparts = 1
         self._bufs.parts = nparts
         if forced_choice is None or eps_tape is None:
@@ -272,10 +256,10 @@ class RolloutGPU:
         _lib.check(L.mhppo_rollout_begin(self.venv.handle, ctypes.byref(mc), _lib.ptr(self.u), _lib.ptr(fa),
                                          ctypes.byref(self._bufs), st))
         if graph is None:  # the default: the one-chain loop (and with MHPPO_ROLLOUT_GRAPH=2 the parts loop)
-            graph = bool(self.use_graph) and (nparts == 1 or fused or self.use_graph == 2)
+            graph = bool(self.use_graph) and (nparts == 1 or self.use_graph == 2)
         graph = bool(graph) and dev.type == "cuda"
         if step_events is None and graph:
-            # The step loop's launches (one chain: 80 fused or 160; parts: 160 per part on their
+            # The step loop's launches (one chain: 160; parts: 160 per part on their
             # streams, forked from and joined back to the capture stream) as one captured HIP
             # graph, replayed: the same kernels and arguments (the pointers, step indices and the
             # actors' mean / std are baked into the graph's nodes and key it), without the
@@ -286,7 +270,7 @@ class RolloutGPU:
             # device was current at its first use, and a launch on another device's stream would
             # run eagerly outside the capture (an empty graph, replayed silently).  The replay
             # goes to dev's current stream, ordered after mhppo_rollout_begin above.
-            key = (fused, nparts, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
+            key = (nparts, mx.packed, mw.packed, mx.mean, mx.std, mw.mean, mw.std)
             with torch.cuda.device(dev):
                 g = self._graphs.get(key)
                 if g is None:
@@ -296,16 +280,16 @@ class RolloutGPU:
                     with torch.cuda.graph(g, stream=self._cap_stream):
                         cap = torch.cuda.current_stream(dev)
                         assert cap == self._cap_stream, "graph capture must run on the env's device"
-                        if fused or nparts == 1:
-                            self._step_loop(L, mx, mw, fused, cap.cuda_stream, None)
+                        if nparts == 1:
+                            self._step_loop(L, mx, mw, cap.cuda_stream, None)
                         else:
                             self._parts_loop(L, mx, mw, nparts, cap)
                     if len(self._graphs) > 8:
                         self._graphs.clear()
                     self._graphs[key] = g
                 g.replay()
-        elif fused or nparts == 1:
-            self._step_loop(L, mx, mw, fused, st, step_events)
+        elif nparts == 1:
+            self._step_loop(L, mx, mw, st, step_events)
         else:
             self._parts_loop(L, mx, mw, nparts, torch.cuda.current_stream(dev))
         del tc, tx, tw, fa  # keep the packed weights alive until the launches are queued

@@ -75,8 +75,11 @@ def test_policy_heads_vs_torch_batch1(case):
         with open(os.path.join(out, f"policy_torch_{v}.json"), "w") as f:
             json.dump(rec, f, indent=1)
     print(json.dumps(rec))
+    # probabilities: float32 rounding of two different summation orders, relative to p (recorded:
+    # 1.4e-6 at config 3, 2.7e-5 at config 4, whose dc = 54 sums are longer; profiles/r05_policy_torch/)
     assert rel <= 1e-4, f"choice probabilities differ by {rel:.3g} relative"
-    assert rec["flips"] == 0 or float(margins.max()) <= 1e-6, rec
+    # every recorded run drew 0 flips (smallest margins 6.0e-7 / 1.2e-6): a flip is a regression
+    assert rec["flips"] == 0, rec
 
     # ---- continuous heads: the step's action a = min(2, mu) + L eps on a sample of rows
     T = ro.T

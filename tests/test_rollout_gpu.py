@@ -111,25 +111,42 @@ def test_rollout_is_shard_invariant():
         assert np.array_equal(a[k], np.concatenate([parts[0][k], parts[1][k]])), k
 
 
-@pytest.mark.parametrize("case", [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 2, 4), ("stop", 2, 2, 2)])
-def test_mfma_policy_bit_identical_to_valu(case):
-    """The MFMA policy kernel (k_policy_mfma: permuted weight rows so every f32-MFMA fmaf
-    chain runs in ascending input order) and the VALU one (k_policy_sorted) give the same
-    episode bit for bit, ragged last tiles included (N*S*P not a multiple of 32)."""
-    from mhppo.env import VecCrosswalk
-    from mhppo.models import Model_PPO
-    from mhppo.rollout import RolloutGPU
-    v, nc, npd, nl = case
-    outs = []
-    for valu in (False, True):
-        ro = RolloutGPU(VecCrosswalk(v, 300, nc, npd, nl, seed_base=777), valu_policy=valu)
-        torch.manual_seed(5)
-        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
-        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
-        ad = Model_PPO(ro.dc, 2, 2).cuda()
-        outs.append(_gpu_out(ro.collect(ac, aw, ad, seed=2, iteration=1)))
-    for k in outs[0]:
-        assert np.array_equal(outs[0][k], outs[1][k]), k
+POLICY_CASES = [("4cars", 4, 1, 2), ("coop", 2, 1, 2), ("scalable", 8, 2, 4), ("stop", 2, 2, 2)]
+
+
+@pytest.mark.parametrize("mode", ["sorted", "unsorted"])
+def test_mfma_policy_bit_identical_to_valu(mode, tmp_path):
+    """The shipped MFMA policy kernel (k_policy_mfma: permuted weight rows so every f32-MFMA fmaf
+    chain runs in ascending input order) and the VALU reference kernels (k_policy_sorted, head-sorted
+    SGPR weights; k_policy, one lane per row), which only the test build of the library carries
+    (tests/lib/libmhppo_test.so, run in a child process), give the same episode bit for bit, ragged
+    last tiles included (N*S*P not a multiple of 32)."""
+    import subprocess
+    import sys
+    from rollout_policy_case import run_case
+    here = os.path.dirname(os.path.abspath(__file__))
+    test_lib = os.path.join(here, "lib", "libmhppo_test.so")
+    assert os.path.exists(test_lib), "build the test library: make -C mh-ppo_amd/csrc test-lib"
+    out = str(tmp_path / "valu.npz")
+    env = dict(os.environ, MHPPO_LIB=test_lib)
+    subprocess.run([sys.executable, os.path.join(here, "valu_policy_worker.py"), out, mode] +
+                   [",".join(map(str, c)) for c in POLICY_CASES], env=env, check=True, timeout=300)
+    valu = np.load(out)
+    for case in POLICY_CASES:
+        mfma = run_case(case, False)
+        cs = ",".join(map(str, case))
+        for k, x in mfma.items():
+            assert np.array_equal(x, valu[f"{cs}/{k}"]), (case, k)
+
+
+def test_valu_policy_refused_by_the_shipped_library():
+    """The shipped library has no VALU policy kernels: asking for them is an error, not a fallback."""
+    from mhppo import _lib
+    from rollout_policy_case import run_case
+    if os.environ.get("MHPPO_LIB"):
+        pytest.skip("an alternative library build is loaded")
+    with pytest.raises(_lib.MhppoError, match="test build only"):
+        run_case(("coop", 2, 1, 2), True)
 
 
 def test_kernel_timing_events_leave_results_unchanged():
@@ -174,7 +191,7 @@ def test_two_part_rollout_equals_one_chain(case):
     outs = []
     for parts in (1, 2):
         venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=900)
-        ro = RolloutGPU(venv, parts=parts, fused=False)
+        ro = RolloutGPU(venv, parts=parts)
         torch.manual_seed(3)
         ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
         aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
@@ -188,46 +205,8 @@ def test_two_part_rollout_equals_one_chain(case):
         assert torch.equal(outs[0][k], outs[1][k]), k
 
 
-@pytest.mark.parametrize("case", [("4cars", 4, 1, 2, 300), ("coop", 2, 1, 2, 1000), ("scalable", 8, 1, 4, 257),
-                                  ("stop", 2, 1, 2, 130), ("4cars", 4, 1, 2, 8192)])
-def test_fused_step_equals_two_launches(case):
-    """mhppo_rollout_step_fused (RolloutGPU(fused=True): the actors' forward on f32 MFMA inside the
-    env-step launch, rows compacted by head per wave) gives bit-identical records, policy outputs
-    and env state to the policy + sample_env launches — ragged N (a partial last wave) included."""
-    from mhppo.env import VecCrosswalk
-    from mhppo.models import Model_PPO
-    from mhppo.rollout import RolloutGPU
-    v, nc, npd, nl, N = case
-    outs = []
-    for fused in (False, True):
-        venv = VecCrosswalk(v, N, nc, npd, nl, seed_base=321)
-        ro = RolloutGPU(venv, parts=1, fused=fused)
-        assert ro.fused_ok and ro.fused == fused
-        torch.manual_seed(8)
-        ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
-        aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
-        ad = Model_PPO(ro.dc, 2, 2).cuda()
-        b = ro.collect(ac, aw, ad, seed=4, iteration=2)
-        torch.cuda.synchronize()
-        outs.append({k: getattr(b, k).clone() for k in ("a_d", "closest", "exist", "obs_c", "act", "logp", "rew",
-                                                         "ep_min", "feat_d", "logp_d")})
-        outs[-1]["out_c"] = ro.out_c.clone()
-        outs[-1]["state"] = venv.state_dict()["blob"]
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
-
-
-def test_fused_supported_shapes():
-    """mhppo_rollout_fused_supported: 1 for the one-pedestrian register-view shapes, 0 otherwise
-    (P = 2 runs the two launches)."""
-    from mhppo.env import VecCrosswalk
-    from mhppo.rollout import RolloutGPU
-    assert RolloutGPU(VecCrosswalk("4cars", 64, 4, 1, 2)).fused_ok
-    assert not RolloutGPU(VecCrosswalk("coop", 64, 2, 2, 2)).fused_ok
-
-
-@pytest.mark.parametrize("fused,parts,N", [(False, 1, 1000), (True, 1, 1000), (False, 2, 4000)])
-def test_graph_replay_equals_eager(fused, parts, N):
+@pytest.mark.parametrize("parts,N", [(1, 1000), (2, 4000)])
+def test_graph_replay_equals_eager(parts, N):
     """RolloutGPU.collect(graph=True): the one-chain step loop captured once as a HIP graph and
     replayed gives bit-identical records and env state to the eager launches — over two
     iterations with new noise and with the actors' weights changed in place in between (the graph
@@ -238,7 +217,7 @@ def test_graph_replay_equals_eager(fused, parts, N):
     outs = []
     for graph in (False, True):
         venv = VecCrosswalk("coop", N, 2, 1, 2, seed_base=77)
-        ro = RolloutGPU(venv, parts=parts, fused=fused)
+        ro = RolloutGPU(venv, parts=parts)
         torch.manual_seed(9)
         ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
         aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()

@@ -6,6 +6,9 @@ the exact f32-MFMA one (exact_f32) — against a float64 torch autograd of
 the same losses (train_model_c, Coop-MH-PPO-scalable.py:778-815) on the same weights.
 Bar: max|dg| <= 1e-4 max|g| for every gradient; the loss sums within 1e-6 relative (the
 advantage sum, which cancels, within 1e-6 of sum|A|)."""
+import json
+import os
+
 import pytest
 import torch
 
@@ -90,6 +93,89 @@ def test_fused_epoch_at_bench_scale_vs_float64_autograd(exact):
     g64 = _flat_grad(a64, surr.sum() / m)
     assert float((ga.double() - g64).abs().max()) <= 1e-4 * float(g64.abs().max())
     assert abs(float(sa[0]) - float(surr.sum())) <= 1e-6 * float(surr.abs().sum())
+
+
+def _follow(r, A):
+    """Which rows' gradient follows r in -min(rA, clamp(r, .8, 1.2) A) (torch's tie rule: the
+    in-range tie gives A): A > 0 up to r = 1.2, A < 0 from r = 0.8 on."""
+    return torch.where(A > 0, r <= 1.2, torch.where(A < 0, r >= 0.8, torch.zeros_like(r, dtype=torch.bool)))
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["bf16x3", "exact_f32"])
+def test_actor_clip_at_bench_scale_vs_float64_autograd(exact):
+    """The continuous actor pass on the bench's 10.5 M-row cross bucket with the actor's weights
+    moved away from the ones that produced logp_old (as after some epochs), so the ratio spreads
+    well past the clip bounds 0.8 / 1.2 (Coop-MH-PPO-scalable.py:803-806): the kernel's gradient
+    against a float64 autograd with the reference's float64 ratio, at the 1e-4 max|g| bar.
+    The kernel takes the clip branch from the float64 difference lp - logp_old
+    (rollout_dev.h surr_and_grad_fd); the test also counts, on torch's float32 lp of the same
+    weights, the rows whose branch a float32 ratio expf(lp - logp_old) would flip against the
+    float64 one, and the rows whose branch float32 lp itself moves against float64 lp (present in
+    the reference too, whose actor is float32) — printed, recorded in DESIGN.md §5."""
+    import math
+    from mhppo import ppo
+    from mhppo.algo import Algo_PPO
+    from mhppo.env import VecCrosswalk
+    from mhppo.models import Model_PPO
+    from mhppo.rollout import bucket_segments
+    venv = VecCrosswalk("4cars", 65536, 4, 1, 2, seed_base=0)
+    torch.manual_seed(0)
+    algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
+    with torch.no_grad():
+        batch = algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0)
+    c, _, _ = bucket_segments(batch)
+    obs, act, lp, ret = c["obs"], c["act"], c["logp"], c["ret"]
+    M = obs.shape[0]
+    assert M > 5_000_000
+    m = float(M)
+    critic, actor = algo.critic_net_cross, algo.actor_net_cross
+    _, sc, V = ppo.k_mlp_train(ppo.KIND_CRITIC, critic, obs, ret, m_global=m, exact=exact)
+    stats = sc[1:3].clone()
+    V = V.clone()
+    g = torch.Generator(device=obs.device).manual_seed(1)
+    with torch.no_grad():  # the actor after some updates: every weight moved, the output shifted
+        for prm in actor.parameters():
+            prm.add_(torch.randn(prm.shape, generator=g, device=prm.device) * 0.1 * prm.abs().mean())
+        actor.layer4.bias.add_(0.1)
+    ga, sa, _ = ppo.k_mlp_train(ppo.KIND_CONT, actor, obs, ret, V, act, lp, stats, m_global=m, exact=exact)
+    ga, sa = ga.clone(), sa.clone()
+    a64 = _f64(actor)
+    mean = float(stats[0]) / m
+    std = ((float(stats[1]) - float(stats[0]) * mean) / (m - 1)) ** 0.5
+    A = ((ret.double() - V.double()) - mean) / (std + 1e-10)
+    half_logdet = 0.5 * math.log(0.5)
+    mu = torch.squeeze(a64(obs.double()), -1)
+    x = (act.double() - mu) / (0.5 ** 0.5)
+    logp = -0.5 * (x * x + math.log(2 * math.pi)) - half_logdet
+    r = torch.exp(logp - lp.double())
+    clipped = float(((r < 0.8) | (r > 1.2)).double().mean())
+    assert 0.2 < clipped < 0.95, f"ratio spread: {clipped:.3f} of rows outside [0.8, 1.2]"
+    surr = -torch.minimum(r * A, r.clamp(0.8, 1.2) * A)
+    g64 = _flat_grad(a64, surr.sum() / m)
+    err = float((ga.double() - g64).abs().max()) / float(g64.abs().max())
+    assert err <= 1e-4, err
+    assert abs(float(sa[0]) - float(surr.sum())) <= 1e-6 * float(surr.abs().sum())
+    # branch flips, on torch's float32 forward of the same weights (the kernel's lp is not exported)
+    with torch.no_grad():
+        mu32 = torch.squeeze(actor(obs), -1)
+        x32 = (act - mu32) * torch.tensor(1.0 / 0.5 ** 0.5, dtype=torch.float32)
+        lp32 = (-0.5 * (x32 * x32 + torch.tensor(math.log(2 * math.pi), dtype=torch.float32))
+                - torch.tensor(half_logdet, dtype=torch.float32))
+        A32 = A.float()
+        f_r32 = _follow(torch.exp(lp32 - lp).double(), A32)       # float32 ratio
+        f_r64 = _follow(torch.exp(lp32.double() - lp.double()), A32)  # float64 ratio, float32 lp
+        f_64 = _follow(r, A32)                                      # float64 ratio, float64 lp
+    flips_ratio = int((f_r32 != f_r64).sum())
+    flips_lp = int((f_r64 != f_64).sum())
+    rec = dict(kernel="exact_f32" if exact else "bf16x3", lib=os.environ.get("MHPPO_LIB") or "in-tree", rows=M,
+               outside_clip=clipped, grad_max_rel_err=err, flips_float32_ratio_vs_float64=flips_ratio,
+               flips_float32_lp_vs_float64_lp=flips_lp)
+    print("\n" + json.dumps(rec))
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        tag = os.path.basename(os.path.dirname(os.environ["MHPPO_LIB"])) if os.environ.get("MHPPO_LIB") else "tree"
+        with open(os.path.join(out, f"clip_scale_{rec['kernel']}_{tag}.json"), "w") as f:
+            json.dump(rec, f, indent=1)
 
 
 def _pair_vs_passes(critic, actor, obs, ret, act, lp, m):

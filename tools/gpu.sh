@@ -18,7 +18,7 @@ TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 summ() {  # one summary line of a bench JSON
-  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d['roofline'];e=d['roofline_env'];print(sys.argv[2], round(d['ms_per_step'],3), 'ms', round(d['value']/1e6,2), 'M/s train', round(r['launch_ms'],4), 'ms', round(r['frac'],4), 'env', round(e['kernel_ms']*1e3,2), 'us', round(e['frac'],4), 'step', round(d['rollout_step_us']['product'],1), 'us')" "$1" "$2"
+  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d['roofline'];e=d['roofline_env'];print(sys.argv[2], round(d['ms_per_step'],3), 'ms', round(d['value']/1e6,2), 'M/s train', round(r['launch_ms'],4), 'ms', round(r['frac'],4), 'env', round(e['kernel_ms']*1e3,2), 'us', round(e['frac'],4), 'step', round(d['rollout_step_us']['product'],1), 'us', 'iters', min(d.get('iter_ms',[0])), '..', max(d.get('iter_ms',[0])))" "$1" "$2"
 }
 for arg in "$@"; do for step in ${arg//,/ }; do
   key=${step%%=*}; val=${step#*=}; [ "$key" = "$step" ] && val=""
