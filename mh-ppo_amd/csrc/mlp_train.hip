@@ -754,22 +754,20 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
 // of the same image.  Weight gradients sum over the tile's 32 rows: both operands go
 // through one per-wave bf16 image [row][feature] of the split parts, read back transposed.
 // Bias gradients and dW4 are f32 row sums through the same LDS slot.
-#ifndef MHPPO_X3_FLOSS
-// the continuous actor's ratio magnitude r = expf(lp - logp_old) in float32, its clip branch
-// decided on the float64 difference lp - logp_old (surr_and_grad_fd: the reference's float64
-// ratio's decision, Coop-MH-PPO-scalable.py:803-806), instead of a float64 exp (A/B builds
-// override).  The float64 exp's temporaries are what kept W3's forward fragments out of the
-// actor's registers (MHPPO_X3_ACT 63 fits at 512 VGPRs without them): cfg3 iteration -1.4 % over
-// three interleaved bench pairs (profiles/r05_floss/).  Numerics: lp - logp_old in float32 is
-// exact only while the two are within a factor 2 of each other (Sterbenz), which updates do not
-// guarantee row by row, so r carries up to two float32 roundings (~1.2e-7 relative) — the level
-// of the difference mu itself has from the reference's CPU GEMM; the clip decision carries none
-// (DESIGN.md §5).  dmu's product stays float64 with one rounding: a float32 chain of four
-// roundings there moved the 2-rank vs 1-rank nets of tests/test_dp_gpu.py from <= 7.6e-7 to
-// 6.4e-5 (tools/dp_diff.py).  The exact f32 kernel keeps the float64 ratio.
-#define MHPPO_X3_FLOSS 1
-#endif
-constexpr bool X3_FLOSS = MHPPO_X3_FLOSS;
+// The continuous actor's ratio: its magnitude r = expf(lp - logp_old) in float32, its clip branch
+// decided on the float64 difference lp - logp_old (surr_and_grad_fd: the decision of the
+// reference's float64 ratio, Coop-MH-PPO-scalable.py:803-806), not a float64 exp.  The float64
+// exp's temporaries kept W3's forward fragments out of the actor's registers (X3_ACT 63 fits at
+// 510 VGPRs without them): cfg3 iteration -1.4 % over three interleaved bench pairs
+// (profiles/r05_floss/); the float64-exp build on r06 driver-length benches: +1.1 % per iteration
+// and the same gradient to 3 digits at bench scale with 23 % of the rows clipped
+// (profiles/r06_a/).  Numerics: lp - logp_old in float32 is exact only while the two are within a
+// factor 2 of each other (Sterbenz), which updates do not guarantee row by row, so r carries up to
+// two float32 roundings (~1.2e-7 relative) — the level of the difference mu itself has from the
+// reference's CPU GEMM; the clip decision carries none.  dmu's product stays
+// float64 with one rounding: a float32 chain of four roundings there moved the 2-rank vs 1-rank
+// nets of tests/test_dp_gpu.py from <= 7.6e-7 to 6.4e-5 (tools/dp_diff.py).  The exact f32
+// kernel keeps the float64 ratio.
 
 namespace x3 {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1518,21 +1516,14 @@ struct Pass {
         const float diff = (float)((double)slot[G::IN_S1 + j] - (double)mu);
         const float x = diff * MVN_INV_L;
         const float lp = (-0.5f * (MVN_LOG2PI + x * x)) - MVN_HALF_LOGDET;
-        float dmu;
-        if constexpr (X3_FLOSS) {  // the ratio in float32, its clip branch decided in float64
-          const float lpo = slot[G::IN_S1 + 32 + j];
-          const float r = expf(lp - lpo);
-          float dfdr;
-          const float f = surr_and_grad_fd(r, (double)lp - (double)lpo, A, dfdr);
-          if (kh == 0) dsum0 += (double)f;
-          dmu = (float)(inv_m * (double)dfdr * (double)r * (double)x * (double)MVN_INV_L);
-        } else {
-          const double r = exp((double)lp - (double)slot[G::IN_S1 + 32 + j]);
-          double dfdr;
-          const double f = surr_and_grad(r, (double)A, dfdr);
-          if (kh == 0) dsum0 += f;
-          dmu = (float)(inv_m * dfdr * r * (double)x * (double)MVN_INV_L);
-        }
+        // the ratio's magnitude in float32, its clip branch decided in float64 (see the note at
+        // the head of namespace x3)
+        const float lpo = slot[G::IN_S1 + 32 + j];
+        const float r = expf(lp - lpo);
+        float dfdr;
+        const float f = surr_and_grad_fd(r, (double)lp - (double)lpo, A, dfdr);
+        if (kh == 0) dsum0 += (double)f;
+        const float dmu = (float)(inv_m * (double)dfdr * (double)r * (double)x * (double)MVN_INV_L);
         dy0 = (dmu * out_std) * (1.0f - t * t);
       } else {
         // choice actor (train_model_d :818-851): softmax over the pair (as torch: shift by the
@@ -2395,30 +2386,26 @@ __device__ __forceinline__ void fold_partials(PassT &p, const WaveSlot<G> &ws, c
 #define MHPPO_X3_BS 7  // bits: 1 critic passes, 2 actor passes, 4 the fused pair (A/B builds override)
 #endif
 constexpr bool X3_BS_CRITIC = MHPPO_X3_BS & 1, X3_BS_ACTOR = MHPPO_X3_BS & 2, X3_BS_PAIR = MHPPO_X3_BS & 4;
-#ifndef MHPPO_X3_CRIT
 // the 13-input critic pass: bits 0-1 = forward fragments held in registers (1 W2, 2 W3), bit 2 =
-// dW4 in registers, bit 3 = DH2F + XCE ordering (A/B builds override)
+// dW4 in registers, bit 3 = DH2F + XCE ordering
 // 15: dW4 in registers, DH2F + XCE, W2's and W3's forward fragments held (the hand-placed passes
 // have the registers since the forward writes the h images: 509 VGPRs; 12 -> 13 -2.1 %, 13 -> 15
 // -3.5 %, profiles/r05_x3/ab.txt, ab_hf3.txt)
-#define MHPPO_X3_CRIT 15
-#endif
-constexpr int X3_CRIT_HF = MHPPO_X3_CRIT & 3;
-constexpr int X3_CRIT_HB = 3 & ~((MHPPO_X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
-constexpr bool X3_CRIT_W4R = MHPPO_X3_CRIT & 4, X3_CRIT_ORD = MHPPO_X3_CRIT & 8;
-#ifndef MHPPO_X3_ACT
+constexpr int X3_CRIT = 15;
+constexpr int X3_CRIT_HF = X3_CRIT & 3;
+constexpr int X3_CRIT_HB = 3 & ~((X3_CRIT >> 4) & 3);  // bits 4-5: backward fragments NOT held (1 W3^T, 2 W2^T)
+constexpr bool X3_CRIT_W4R = X3_CRIT & 4, X3_CRIT_ORD = X3_CRIT & 8;
 // the continuous actor pass: bits 0-1 = forward fragments held (1 W2, 2 W3), bits 2-3 = backward
-// fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE (A/B overrides)
+// fragments held (1 W3^T, 2 W2^T), bit 4 = dW4 in registers, bit 5 = DH2F + XCE
 // 61: both backward fragments held, dW4 in registers, DH2F + XCE, W2's forward fragments held (485
 // VGPRs since the forward writes the h images; -1.5 % vs 60, profiles/r05_x3/ab.txt); 63: W3's
 // forward fragments too, which fit (512 VGPRs, no spill) only with the float32 loss math
-// (MHPPO_X3_FLOSS; with the float64 ratio 63 spills 60 B)
-#define MHPPO_X3_ACT (MHPPO_X3_FLOSS ? 63 : 61)
-#endif
-constexpr int X3_ACT_HF = MHPPO_X3_ACT & 3, X3_ACT_HB = (MHPPO_X3_ACT >> 2) & 3;
-constexpr bool X3_ACT_W4R = MHPPO_X3_ACT & 16, X3_ACT_ORD = MHPPO_X3_ACT & 32;
+// (with a float64 exp 63 spilled 60 B)
+constexpr int X3_ACT = 63;
+constexpr int X3_ACT_HF = X3_ACT & 3, X3_ACT_HB = (X3_ACT >> 2) & 3;
+constexpr bool X3_ACT_W4R = X3_ACT & 16, X3_ACT_ORD = X3_ACT & 32;
 #ifndef MHPPO_X3_CC
-#define MHPPO_X3_CC 0  // the choice critic (runtime input count), bits as MHPPO_X3_CRIT (A/B overrides)
+#define MHPPO_X3_CC 0  // the choice critic (runtime input count), bits as X3_CRIT (A/B overrides)
 #endif
 #ifndef MHPPO_X3_CA
 #define MHPPO_X3_CA 0  // the choice actor: bits 0-1 forward fragments held, bit 3 DH2F + XCE
@@ -2449,11 +2436,6 @@ __global__ void __launch_bounds__(64 * x3::WAVES)
   prefetch_first<KIND, G>(ws, gw, M, X, nin, ret, V, act, lp_old);
   stage_net<G>(W, L8, tid, nin);
   __syncthreads();
-#ifdef MHPPO_X3_STAGGER
-  // A/B builds only: wave w of the block starts w x MHPPO_X3_STAGGER x 64 cycles late, so the
-  // four waves of a CU reach their LDS-store blocks and input DMA out of phase
-  for (int i = 0; i < w; i++) __builtin_amdgcn_s_sleep(MHPPO_X3_STAGGER);
-#endif
   // the 13-input critic pass alone holds its forward weight fragments in registers (with a
   // runtime input count the choice critic has no registers for them: 23-38 spills)
   constexpr bool C13 = KIND == K_CRITIC && G::NIC == NIN_CONT;  // the 13-input critic
