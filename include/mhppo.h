@@ -321,7 +321,7 @@ int mhppo_ppo_choice_fwd_bwd(const float *probs, const float *logp_old, const fl
  *          float) is read and each row contributes its own action's surrogate / M_global.
  * grad: packed torch layout W1 b1 W2 b2 W3 b3 W4 b4 (32 n_in + 4224 + 33 n_out floats).
  * m_global = the global row count (data parallel: all ranks' rows).
- * Heads with n_in <= 31 run on bf16 MFMA with every f32 operand split exactly into three
+ * Heads with n_in <= 54 run on bf16 MFMA with every f32 operand split exactly into three
  * bf16 parts (products to f32 accuracy; X must then be 16-byte aligned); kind |
  * MHPPO_TRAIN_EXACT_F32 selects the f32-MFMA kernel, whose sums are k-ordered fmaf chains
  * (wider heads always run on it).

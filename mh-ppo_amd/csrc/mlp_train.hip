@@ -493,7 +493,8 @@ __global__ void __launch_bounds__(PF ? 512 : 256)  // 64 * Lay::WAVES
       const float rt = slot[LY::IN_S0 + j];
       if constexpr (KIND == K_CRITIC) {
         const float v = y0;
-        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 128), 4 * j, 0, 0);
+        // the store's range is the tile's rows in the batch: no lane can write past the batch
+        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(V + row0, 4 * nrows), 4 * j, 0, 0);
         const float a = rt - v;
         const float d = v - rt;
         if (kh == 0) {
@@ -790,20 +791,20 @@ constexpr int WAVES = 4;  // one wave per SIMD (512 registers)
 
 // Geometry of one split-precision net: K1 = layer-1 K (the inputs and the bias column, padded to
 // whole 16-deep K-steps), NOUT outputs, NIC the compile-time input count (0: a kernel argument,
-// nin <= K1 - 1).  LDS: the net's weights (bf16 images of W1..W3, f32 b2 b3 w4 b4), then per
-// wave: the tile image (also the f32 transpose image), two input slots (double buffered), a
-// second tile image.
-template <int K1_, int NOUT_, int NIC_, int NIM_ = 2>
+// nin <= NMX, by default K1 - 1).  LDS: the net's weights (bf16 images of W1..W3, f32 b2 b3 w4
+// b4), then per wave: the tile image (also the f32 transpose image), two input slots (double
+// buffered), a second tile image.
+template <int K1_, int NOUT_, int NIC_, int NIM_ = 2, int NMX_ = K1_ - 1>
 struct Geo {
-  static constexpr int K1 = K1_, KS1 = K1 / 16, NOUT = NOUT_, NIC = NIC_, NIM = NIM_;
-  static_assert(K1 % 16 == 0 && (NIC == 0 || NIC < K1), "layer-1 geometry");
+  static constexpr int K1 = K1_, KS1 = K1 / 16, NOUT = NOUT_, NIC = NIC_, NIM = NIM_, NMX = NMX_;
+  static_assert(K1 % 16 == 0 && (NIC == 0 || NIC < K1) && NMX < K1, "layer-1 geometry");
   static constexpr int W1_ROWB = 2 * K1 + 8, W1_PART = 32 * W1_ROWB;
   static constexpr int O_W1 = 0, O_W2 = O_W1 + 3 * W1_PART, O_W3 = O_W2 + 3 * W2_PART, O_F = O_W3 + 3 * W3_PART;
   static constexpr int F_W4 = 96, F_B4 = F_W4 + 32 * NOUT, NF = F_B4 + NOUT;  // f32: b2[64] b3[32] w4 b4
   static constexpr int NET_B = (O_F + NF * 4 + 15) / 16 * 16;
   // input slot (floats): X [32][nin] | s0 [32 | 32] | s1 [32 | 32].  A runtime nin gets an X region
   // of whole 1-KiB pieces, so every LDS-DMA piece lands unmasked (zeros past the rows).
-  static constexpr int XMAX = NIC ? (32 * NIC + 3) / 4 * 4 : (32 * (K1 - 1) + 255) / 256 * 256;
+  static constexpr int XMAX = NIC == NIN_CONT ? (32 * NIC + 3) / 4 * 4 : (32 * (NIC ? NIC : NMX) + 255) / 256 * 256;
   static constexpr int IN_X = 0, IN_S0 = XMAX, IN_S1 = XMAX + 64, IN_SZ = XMAX + 128 + (NIC ? 32 : 0);
   static constexpr int XPIECES = (XMAX * 4 + 1023) / 1024;
   // NIM tile-image slots per wave: slot 1 at 0, slot 2 at O_IM2, slots 3 and 4 after it (the
@@ -822,11 +823,20 @@ using G13S = Geo<16, 1, NIN_CONT, 4>;  // the hand-placed single-net passes (fou
 using LY = Lay<7, true, 1>;
 static_assert(G13::IN_S0 == LY::IN_S0 && G13::IN_S1 == LY::IN_S1 && G13::IN_SZ == LY::IN_SZ, "13-input slot");
 static_assert(G13::LDS_BYTES_PAIR <= 160 * 1024, "LDS budget (pair)");
-// the choice heads' nets on this kernel: up to 31 inputs (wider ones stay on the f32 kernel)
+// the choice heads' nets on this kernel: up to NIN_X3C inputs (wider ones stay on the f32 kernel).
+// K = 64 (the scalable 8-slot env's dc = 54, Coop-MH-PPO-scalable.py:818-851): the input slots sized
+// for 54 inputs (7 KiB of X rows), the four waves' slots and the weights then fit the 160 KiB of LDS
+constexpr int NIN_X3C = 54;
 using GC16 = Geo<16, 2, 0>;
 using GV16 = Geo<16, 1, 0>;
 using GC32 = Geo<32, 2, 0>;
 using GV32 = Geo<32, 1, 0>;
+using GC64 = Geo<64, 2, 0, 2, NIN_X3C>;
+using GV64 = Geo<64, 1, 0, 2, NIN_X3C>;
+// dc = 54 itself with a compile-time input count: the runtime count's address arithmetic spilled
+// the choice actor (15 VGPRs at 512); compile-time: 496 VGPRs, no spill
+using GC54 = Geo<64, 2, 54, 2, 54>;
+using GV54 = Geo<64, 1, 54, 2, 54>;
 
 #ifdef MHPPO_X3_PHASE
 __device__ __forceinline__ void x3_phase() { __builtin_amdgcn_sched_barrier(0); }
@@ -1499,7 +1509,9 @@ struct Pass {
       const float rt = slot[G::IN_S0 + j];
       if constexpr (KIND == K_CRITIC) {
         const float v = y0;
-        if (kh == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 128), 4 * j, 0, 0);
+        // the store's range is the tile's rows in the batch (a wrong row index reaches no memory)
+        if (kh == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(Vout + row0, 4 * nrows), 4 * j, 0, 0);
         const float a = rt - v;
         const float d = v - rt;
         if (kh == 0) {
@@ -2687,8 +2699,8 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
   if (!wkp) return set_error(MHPPO_EINVAL, "train passes on more than %d streams of one device", WORK_STREAMS);
   Work &wk = *wkp;
   const bool split = pf && !exact;  // bf16x3 split-precision kernel (default for the 13-input heads)
-  // the choice heads' nets (up to 31 inputs) on the split-precision kernel too (wider: f32 MFMA)
-  const bool split_c = !pf && !exact && n_in <= 31;
+  // the choice heads' nets (up to NIN_X3C inputs) on the split-precision kernel too (wider: f32 MFMA)
+  const bool split_c = !pf && !exact && n_in <= x3::NIN_X3C;
   if (split_c && ((uintptr_t)X & 15) != 0) return set_error(MHPPO_EINVAL, "X must be 16-byte aligned (LDS-DMA rows)");
   const int waves = (split || split_c) ? x3::WAVES : (pf ? 8 : 4);
   int64_t blocks = wk.cus;  // one block per CU, grid-stride over 32-row tiles
@@ -2709,9 +2721,15 @@ extern "C" int mhppo_mlp_train(int kind, int n_in, const float *packed, const fl
     } else if (n_in <= 15) {
       if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV16);
       else X3_LAUNCH(K_CHOICE, GC16);
-    } else {
+    } else if (n_in <= 31) {
       if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV32);
       else X3_LAUNCH(K_CHOICE, GC32);
+    } else {
+      if (n_in == 54) {
+        if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV54);
+        else X3_LAUNCH(K_CHOICE, GC54);
+      } else if (kind == K_CRITIC) X3_LAUNCH(K_CRITIC, GV64);
+      else X3_LAUNCH(K_CHOICE, GC64);
     }
 #undef X3_LAUNCH
   } else if (pf) {

@@ -212,7 +212,7 @@ def k_mlp_train(kind, net, obs, ret, value=None, act=None, logp_old=None, stats=
     .grad storage.  An empty `obs` (an empty data-parallel shard) gives a zero gradient.
     `sums`: optional zeroed float64 [3] the kernel accumulates into (train_epoch passes rows of
     one zeroed tensor: one fill per epoch instead of one per pass).
-    exact: the f32-MFMA kernel instead of the split-precision one (any head with n_in <= 31;
+    exact: the f32-MFMA kernel instead of the split-precision one (any head with n_in <= 54;
     wider choice heads always run on f32 MFMA)."""
     want = {KIND_CRITIC: 0, KIND_CONT: 1, KIND_CHOICE: 2}[kind]
     if net.model_type != want or net.n_in > N_IN_MAX or (kind == KIND_CONT and net.n_in != 13):

@@ -136,12 +136,12 @@ def test_fused_cont_grads_vs_autograd(M):
 @pytest.mark.parametrize("M,dc,exact", [(1, 12, False), (45, 17, False), (4096, 27, False), (20001, 30, False),
                                         (333, 32, False), (70, 54, False), (65536, 54, False), (1000, 40, False),
                                         (257, 64, False), (20001, 30, True), (4097, 16, True), (100003, 17, False),
-                                        (64, 16, False), (65, 31, False)])
+                                        (64, 16, False), (65, 31, False), (524288, 54, False), (4099, 36, False)])
 def test_fused_choice_grads_vs_autograd(M, dc, exact):
     """mhppo_mlp_train kinds 0/2 on choice-head shapes (dc = 12..64 inputs — 54 is the
     scalable 8-slot driver's choice head, 2-way softmax, O(M) count-weighted surrogate) vs
-    torch autograd + the HIP choice-loss kernel.  dc <= 31 runs on the bf16x3 split kernel
-    (K = 16 / 32 geometries), exact=True and dc > 31 on the f32-MFMA one."""
+    torch autograd + the HIP choice-loss kernel.  dc <= 54 runs on the bf16x3 split kernel
+    (K = 16 / 32 / 64 geometries), exact=True and dc > 54 on the f32-MFMA one."""
     from mhppo import ppo
     from mhppo.models import Model_PPO
     torch.manual_seed(M + dc)
