@@ -101,8 +101,8 @@ MHPPO_HD void car_init(EV &E, int s, double line, double offset, int exist) {
   E.car(C_TS, s) = (V == V_SCALABLE) ? 0. : -10.;
   E.hist_nf(0) &= ~(int32_t)(1u << s);  // history = [0, 0]
   E.hist_nf(1) &= ~(int32_t)(1u << s);
-  E.car(C_LINE, s) = line;
-  E.car(C_EXIST, s) = exist ? 1.0 : 0.0;
+  E.set_line(s, line);
+  E.set_exist(s, exist ? 1.0 : 0.0);
 }
 
 // car.get_data for the flat obs (coop :609-612, scalable :652-655)
@@ -110,18 +110,18 @@ template <class EV>
 MHPPO_HD int write_car_obs(const EV &E, int s, float *o) {
   constexpr int V = EV::VAR;
   if (V == V_SCALABLE) {
-    if (E.car(C_EXIST, s) == 0.0) {
-      o[0] = 0.f; o[1] = 0.f; o[2] = 10.f; o[3] = -1000.f; o[4] = 0.f; o[5] = (float)E.car(C_LINE, s); o[6] = 0.f;
+    if (E.exists(s) == 0.0) {
+      o[0] = 0.f; o[1] = 0.f; o[2] = 10.f; o[3] = -1000.f; o[4] = 0.f; o[5] = (float)E.line(s); o[6] = 0.f;
     } else {
       double Vc = E.car(C_VC, s);
       o[0] = (float)E.car(C_AC, s); o[1] = (float)Vc; o[2] = (float)(10.0 - Vc); o[3] = (float)E.car(C_SC, s);
-      o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.car(C_LINE, s); o[6] = 1.f;
+      o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.line(s); o[6] = 1.f;
     }
     return 7;
   }
   double Vc = E.car(C_VC, s);
   o[0] = (float)E.car(C_AC, s); o[1] = (float)Vc; o[2] = (float)(10.0 - Vc); o[3] = (float)E.car(C_SC, s);
-  o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.car(C_LINE, s);
+  o[4] = (float)E.car(C_LIGHT, s); o[5] = (float)E.line(s);
   return 6;
 }
 
@@ -214,7 +214,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   } else {
     for (int i = 0; i < c.nb_car; i++) car_init(E, i, (double)(i % c.nb_lines), 0, 1);
     if (has_followers(V))
-      for (int i = 0; i < c.nb_car; i++) car_init(E, c.nAV + i, E.car(C_LINE, i), 0, 1);
+      for (int i = 0; i < c.nb_car; i++) car_init(E, c.nAV + i, E.line(i), 0, 1);
   }
   b.envi[sidx(EI_NI, EI_CARTRAF, e)] = car_traffic;
   int ped_traffic = E.rng.randint(1, c.nb_ped);
@@ -230,7 +230,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
       E.car(C_SC, c.nAV + i) = E.car(C_SC, i) - gap;
       E.car(C_VC, c.nAV + i) = 10.0;
       E.car(C_LIGHT, c.nAV + i) = 0.;
-      E.car(C_LINE, c.nAV + i) = E.car(C_LINE, i);
+      E.set_line(c.nAV + i, E.line(i));
     }
   }
   env_observe(E, 0, obs);
@@ -252,7 +252,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
 template <int V>
 MHPPO_HD void env_choix_test_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   Env<V> E(c, b, e);
-  const double v0 = (double)(float)(E.car(C_EXIST, 0) != 0.0 ? E.car(C_VC, 0) : 0.0);
+  const double v0 = (double)(float)(E.exists(0) != 0.0 ? E.car(C_VC, 0) : 0.0);
   E.cross = 3.0;
   E.cl = (double)c.nb_lines * E.cross;
   b.envd[sidx(E_ND, E_CROSS, e)] = E.cross;
@@ -288,8 +288,8 @@ MHPPO_HD void env_choix_test_one(const Cfg &c, const Bufs &b, int e, float *obs)
     q.W = PI / T;
   }
   store_ped(E, 0, q, false);
-  E.car(C_SC, 0) = -45.0; E.car(C_VC, 0) = v0; E.car(C_LIGHT, 0) = 0.0; E.car(C_LINE, 0) = 0.0;
-  E.car(C_SC, 1) = -22.0; E.car(C_VC, 1) = v0; E.car(C_LIGHT, 1) = 0.0; E.car(C_LINE, 1) = 1.0;
+  E.car(C_SC, 0) = -45.0; E.car(C_VC, 0) = v0; E.car(C_LIGHT, 0) = 0.0; E.set_line(0, 0.0);
+  E.car(C_SC, 1) = -22.0; E.car(C_VC, 1) = v0; E.car(C_LIGHT, 1) = 0.0; E.set_line(1, 1.0);
   env_observe(E, 0, obs);
   if (obs) {  // get_data shows ped_left / ped_in_cross as stored: -1 and 3.0
     float *o = obs + (size_t)e * c.obs_dim + (c.obs_dim - 9 * c.P);
@@ -319,7 +319,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
     double a = act[i];
     if (V == V_SCALABLE) {
       double idm = 2.;
-      if (i % 2 == 1 && E.car(C_EXIST, i - 1) != 0.0 && E.car(C_EXIST, i) != 0.0)
+      if (i % 2 == 1 && E.exists(i - 1) != 0.0 && E.exists(i) != 0.0)
         idm = car_follow_action(E, i, E.car(C_VC, i - 1), E.car(C_SC, i - 1));
       a = pymin(idm, a);
     }
@@ -379,7 +379,7 @@ MHPPO_HD void env_step_body(EV &E, const ACT &act, float *obs, uint8_t *done) {
         uint32_t fl = E.pflag(p);
         if (!(fl & F_EXIST)) continue;
         Ped q = load_ped(E, p);
-        double w = new_reward_wait_safety(E, q, Vc, E.car(C_SC, i), E.car(C_LINE, i));
+        double w = new_reward_wait_safety(E, q, Vc, E.car(C_SC, i), E.line(i));
         E.pedf(P_WDL, p) = q.wdl;
         if (!have) { mn = w; have = true; }
         else if (w < mn) mn = w;
@@ -436,7 +436,7 @@ MHPPO_HD void env_state_one(const Cfg &c, const Bufs &b, int e, double *out, int
   }
   for (int s = 0; s < c.nC; s++) {
     double f[8] = {E.car(C_AC, s), E.car(C_VC, s), E.car(C_SC, s), E.car(C_LIGHT, s),
-                   E.car(C_PA, s), E.car(C_ES, s), E.car(C_TS, s), E.car(C_EXIST, s)};
+                   E.car(C_PA, s), E.car(C_ES, s), E.car(C_TS, s), E.exists(s)};
     for (int j = 0; j < 8; j++) o[k++] = f[j];
   }
   o[k++] = E.cross;

@@ -158,7 +158,13 @@ struct Bufs {
   int32_t *envi;  // [N/EB][EI_NI][EB]
   uint32_t *mt;   // [N][2][624] (active + next block, see RngT)
   uint32_t *ev;   // [N/EB][EV_N][EB] event counters (touched only when an event fires)
+  // [N][2][nC] bytes: every car slot's line and existence, the static car fields (the step never
+  // writes them; reset and choix_test do, through Env::set_line / set_exist, which keep car's
+  // C_LINE / C_EXIST doubles and these bytes equal).  The register view reads only the bytes:
+  // 2 nC bytes per env and step instead of 16 nC (one 16-B load per lane at nC = 8)
+  uint8_t *carb;
 };
+MHPPO_HD __forceinline__ size_t carb_idx(int nC, int f, int s, int e) { return ((size_t)e * 2 + f) * nC + s; }
 
 // Env-blocked state layout: every field array ([rows] per env: car C_NF*nC, ped P_NF*P,
 // flags P, envd E_ND, envi EI_NI) is stored [ceil(N/EB)][rows][EB], so one wave's 64 envs
@@ -457,6 +463,17 @@ struct Env {
   MHPPO_HD int32_t &hist_nf(int k) const { return b.envi[sidx(EI_NI, EI_H0NF + k, e)]; }
 
   MHPPO_HD double &car(int f, int s) const { return b.car[sidx(C_NF * c.nC, f * c.nC + s, e)]; }
+  // the static car fields: read here from the doubles, written to the doubles and the byte mirror
+  MHPPO_HD double line(int s) const { return car(C_LINE, s); }
+  MHPPO_HD double exists(int s) const { return car(C_EXIST, s); }
+  MHPPO_HD void set_line(int s, double v) const {
+    car(C_LINE, s) = v;
+    b.carb[carb_idx(c.nC, 0, s, e)] = (uint8_t)v;
+  }
+  MHPPO_HD void set_exist(int s, double v) const {
+    car(C_EXIST, s) = v;
+    b.carb[carb_idx(c.nC, 1, s, e)] = (uint8_t)v;
+  }
   MHPPO_HD double &pedf(int f, int p) const { return b.ped[sidx(P_NF * c.P, f * c.P + p, e)]; }
   MHPPO_HD uint32_t &pflag(int p) const { return b.pfl[sidx(c.P, p, e)]; }
   MHPPO_HD void event(int k) const { ev_inc(&b.ev[sidx(EV_N, k, e)]); }
@@ -533,7 +550,9 @@ struct EnvR {
   int e;
   RngT<MHPPO_RNG_WIN> rng;
   double cross, cl;
-  mutable double car_[C_NF][NC];
+  mutable double car_[C_LINE][NC];  // the dynamic car fields (C_LINE and C_EXIST come from carb)
+  static constexpr int NCB = (2 * NC + 3) / 4;
+  double st_[2][NC];  // line, exist of every slot, decoded once from carb's 2 NC bytes
   mutable double ped_[P_NF][NP];
   mutable uint32_t pfl_[NP];
   mutable int32_t hnf_[2];
@@ -549,9 +568,22 @@ struct EnvR {
     hnf_[0] = b.envi[sidx(EI_NI, EI_H0NF, e)];
     hnf_[1] = b.envi[sidx(EI_NI, EI_H1NF, e)];
 #pragma unroll
-    for (int f = 0; f < C_NF; f++)
+    for (int f = 0; f < C_LINE; f++)
 #pragma unroll
       for (int s = 0; s < NC; s++) car_[f][s] = b.car[sidx(C_NF * NC, f * NC + s, e)];
+    uint32_t cb[NCB];  // packed: line of slot s = byte s, exist = byte NC + s
+    if constexpr ((2 * NC) % 4 == 0) {  // whole dwords (one 16-B load at NC = 8)
+      const uint32_t *cw = reinterpret_cast<const uint32_t *>(b.carb + carb_idx(NC, 0, 0, e));
+#pragma unroll
+      for (int k = 0; k < NCB; k++) cb[k] = cw[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCB; k++) cb[k] = 0u;
+#pragma unroll
+      for (int k = 0; k < 2 * NC; k++) cb[k / 4] |= (uint32_t)b.carb[carb_idx(NC, 0, k, e)] << (8 * (k % 4));
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * NC; k++) st_[k / NC][k % NC] = (double)((cb[k / 4] >> (8 * (k % 4))) & 0xffu);
 #pragma unroll
     for (int f = 0; f < P_NF; f++)
 #pragma unroll
@@ -620,6 +652,8 @@ struct EnvR {
   MHPPO_HD int car_traffic() const { return ctraf; }
 
   MHPPO_HD double &car(int f, int s) const { return car_[f][s]; }
+  MHPPO_HD double line(int s) const { return st_[0][s]; }
+  MHPPO_HD double exists(int s) const { return st_[1][s]; }
   MHPPO_HD int32_t &hist_nf(int k) const { return hnf_[k]; }
   MHPPO_HD double &pedf(int f, int p) const { return ped_[f][p]; }
   MHPPO_HD uint32_t &pflag(int p) const { return pfl_[p]; }
@@ -692,7 +726,7 @@ template <class EV>
 MHPPO_HD inline bool in_view(const EV &E, int s, int mode) {
   constexpr int V = EV::VAR;
   if (has_followers(V)) return mode == 1 || s < E.nAV();
-  if (V == V_SCALABLE) return mode == 0 || E.car(C_EXIST, s) != 0.0;
+  if (V == V_SCALABLE) return mode == 0 || E.exists(s) != 0.0;
   return true;
 }
 
@@ -741,7 +775,7 @@ MHPPO_HD inline bool choix_pedestrian(EV &E, const Ped &q, int mode) {
       // naif: view == all slots, in order
       for (int k = 0; k < n; k++) {
         int i = (int)((perm >> (4 * k)) & 15u);
-        double pos = E.car(C_SC, i), line = E.car(C_LINE, i);
+        double pos = E.car(C_SC, i), line = E.line(i);
         if (is_crossing_in_front(E, q, line, 0.5) && is_in_front(E, q, line, 1.0) &&
             (pos < car_size + q.Sx) && (pos > q.Sx))
           return false;
@@ -756,7 +790,7 @@ MHPPO_HD inline bool choix_pedestrian(EV &E, const Ped &q, int mode) {
       MHPPO_UNROLL
       for (int s = 0; s < E.nC(); s++) {
         if (!in_view(E, s, mode)) continue;
-        double pos = E.car(C_SC, s), line = E.car(C_LINE, s);
+        double pos = E.car(C_SC, s), line = E.line(s);
         if (is_crossing_in_front(E, q, line, 0.5) && is_in_front(E, q, line, 1.0)) {
           if ((pos < car_size + q.Sx) && (pos > q.Sx)) return false;
         }
@@ -781,7 +815,7 @@ MHPPO_HD inline bool choix_pedestrian(EV &E, const Ped &q, int mode) {
     MHPPO_UNROLL
     for (int s = E.nC() - 1; s >= 0; s--) {  // descending: the lowest qualifying slot wins
       if (s < from || !in_view(E, s, mode)) continue;
-      const double ln = E.car(C_LINE, s), ps = E.car(C_SC, s);
+      const double ln = E.line(s), ps = E.car(C_SC, s);
       if (!is_in_front(E, q, ln, 1.0)) continue;
       if (((ps < car_size + q.Sx) && (ps > q.Sx)) || (ps < q.Sx)) {
         hit = s;
@@ -828,7 +862,7 @@ MHPPO_HD inline double delta_l_all(const EV &E, const Ped &q, int mode) {
   for (int s = 0; s < E.nC(); s++) {
     if (!in_view(E, s, mode)) continue;
     double pos = E.car(C_SC, s), spd = E.car(C_VC, s);
-    if ((pos <= q.Sx) && is_in_front(E, q, E.car(C_LINE, s), 0) && (!q.has(F_LEFT)) && (E.car(C_LIGHT, s) >= 0)) {
+    if ((pos <= q.Sx) && is_in_front(E, q, E.line(s), 0) && (!q.has(F_LEFT)) && (E.car(C_LIGHT, s) >= 0)) {
       double nd = fabs(pos - q.Sx) - brake_dist(E, spd) - 1.0 * (spd);
       dl = pymin(dl, nd);
     }
@@ -1023,15 +1057,15 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
   if (V != V_NAIF) {
     MHPPO_UNROLL
     for (int k = 0; k < nS; k++)
-      if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0))
+      if (E.car(C_LIGHT, k) > 0. && E.car(C_SC, k) < q.Sx && (V != V_SCALABLE || E.exists(k) != 0.0))
         clw += 1.0;
   }
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
-    bool cond = is_in_front(E, q, E.car(C_LINE, i), 0);
-    if (V == V_SCALABLE) cond = cond && (E.car(C_EXIST, i) != 0.0);
+    bool cond = is_in_front(E, q, E.line(i), 0);
+    if (V == V_SCALABLE) cond = cond && (E.exists(i) != 0.0);
     if (!cond) continue;
-    double Sc = E.car(C_SC, i), Vc = E.car(C_VC, i), line = E.car(C_LINE, i);
+    double Sc = E.car(C_SC, i), Vc = E.car(C_VC, i), line = E.line(i);
     int ped_accident;
     if (V == V_NAIF) {
       q.set(F_WSA, worst_delta_l(E, q, Sc, Vc, line) < 0);
@@ -1085,14 +1119,14 @@ MHPPO_HD inline void ped_detection(EV &E, Ped &q, const AV &prev, AV &acc, bool 
   double green = 0;
   MHPPO_UNROLL
   for (int k = 0; k < nS; k++)
-    if (E.car(C_LIGHT, k) > 0. && (V != V_SCALABLE || E.car(C_EXIST, k) != 0.0)) green += 1.0;
+    if (E.car(C_LIGHT, k) > 0. && (V != V_SCALABLE || E.exists(k) != 0.0)) green += 1.0;
   MHPPO_UNROLL
   for (int i = 0; i < nS; i++) {
     double res = E.car(C_PA, i) + E.car(C_ES, i);
     double term = 0.5 * green * (double)(E.car(C_LIGHT, i) < 0.) * (double)(E.car(C_TS, i) > 0);
     if (V == V_COOP || V == V_4CARS2 || V == V_STOP) res = res + term;
     else if (V == V_4CARS || V == V_SCALABLE) res = res - term;
-    if (V == V_SCALABLE && E.car(C_EXIST, i) == 0.0) res = 0.;
+    if (V == V_SCALABLE && E.exists(i) == 0.0) res = 0.;
     acc[i] += res;
   }
 }

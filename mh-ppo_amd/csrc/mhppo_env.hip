@@ -137,10 +137,10 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   size_t bytes_car = sizeof(double) * C_NF * c.nC * N, bytes_ped = sizeof(double) * P_NF * c.P * N;
   size_t bytes_pfl = sizeof(uint32_t) * c.P * N, bytes_envd = sizeof(double) * E_ND * N;
   size_t bytes_envi = sizeof(int32_t) * EI_NI * N, bytes_mt = sizeof(uint32_t) * (MT_BLOCKS * MT_N * (size_t)c.N + MT_PAD);
-  size_t bytes_ev = sizeof(uint32_t) * EV_N * N;
+  size_t bytes_ev = sizeof(uint32_t) * EV_N * N, bytes_carb = (size_t)2 * c.nC * N;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t total = al(bytes_car) + al(bytes_ped) + al(bytes_pfl) + al(bytes_envd) + al(bytes_envi) + al(bytes_ev) +
-                 al(bytes_mt);
+                 al(bytes_carb) + al(bytes_mt);
   if (hipMalloc(&h->blob, total) != hipSuccess) {
     delete h;
     return set_error(MHPPO_ENOMEM, "hipMalloc(%zu) failed", total);
@@ -153,6 +153,7 @@ int mhppo_env_create(const mhppo_env_cfg *cfg, int device, mhppo_env **out) {
   h->b.envd = (double *)p; p += al(bytes_envd);
   h->b.envi = (int32_t *)p; p += al(bytes_envi);
   h->b.ev = (uint32_t *)p; p += al(bytes_ev);
+  h->b.carb = (uint8_t *)p; p += al(bytes_carb);
   h->b.mt = (uint32_t *)p;
   // any failure past the allocation releases the blob and the handle before reporting
   hipError_t e = hipMemset(h->blob, 0, total);

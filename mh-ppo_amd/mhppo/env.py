@@ -143,9 +143,10 @@ class VecCrosswalk:
                 [float(x) for x in c.cross_b], int(c.seed_base), int(c.env_id_offset)]
 
     # Layout version of the exported device blob (mhppo_env_export): bump whenever the blob's
-    # layout changes, even at the same size.  2 = r03 layout (event counters before the MT blocks,
-    # the 4-block MT19937 ring, EI_MTB = active block + stale bits); 1 = r02 (2 MT blocks).
-    STATE_LAYOUT = 2
+    # layout changes, even at the same size.  3 = r06 layout (the cars' line / existence bytes,
+    # Bufs.carb, between the event counters and the MT blocks); 2 = r03 layout (event counters before
+    # the MT blocks, the 4-block MT19937 ring, EI_MTB = active block + stale bits); 1 = r02 (2 MT blocks).
+    STATE_LAYOUT = 3
 
     def state_dict(self):
         """Whole device state (all env fields + every env's MT19937 stream), for exact resume."""

@@ -14,7 +14,7 @@ def run_case(case, valu_policy):
     ac = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
     aw = Model_PPO(13, 1, 1, mean=-1.0, std=3.0).cuda()
     ad = Model_PPO(ro.dc, 2, 2).cuda()
-    b = ro.collect(ac, aw, ad, seed=2, iteration=1)
+    b = ro.collect(ac, aw, ad, seed=2, iteration=1, graph=False)
     out = {k: getattr(b, k).cpu().numpy() for k in ("feat_d", "a_d", "logp_d", "closest", "exist", "obs_c", "act",
                                                       "logp", "rew", "ep_min")}
     return out

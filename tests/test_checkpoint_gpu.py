@@ -41,8 +41,9 @@ def test_resume_is_bit_identical(tmp_path, monkeypatch):
     assert (tmp_path / "load_model" / "parameters").is_dir()  # train() wrote the reward curves (:908-916)
 
 
-def test_keyless_env_checkpoint_loads_as_layout_2():
-    # an r03 env checkpoint has no "layout" key; its blob is layout 2: it must resume
+def test_keyless_env_checkpoint_is_refused():
+    # r02 / r03 env checkpoints carry no "layout" key; their blobs (layouts 1 / 2) lack the cars'
+    # line / existence bytes of layout 3 (r06), so this build refuses them instead of misreading them
     from mhppo.env import VecCrosswalk
     v = VecCrosswalk("coop", 128, 2, 1, 2, seed_base=5)
     v.reset()
@@ -50,6 +51,9 @@ def test_keyless_env_checkpoint_loads_as_layout_2():
     sd = v.state_dict()
     del sd["layout"]
     w = VecCrosswalk("coop", 128, 2, 1, 2, seed_base=5)
+    with pytest.raises(ValueError, match="state layout"):
+        w.load_state_dict(sd)
+    sd["layout"] = VecCrosswalk.STATE_LAYOUT  # the same blob with its layout key resumes exactly
     w.load_state_dict(sd)
     assert torch.equal(v.get_rng()[0], w.get_rng()[0]) and torch.equal(v.get_rng()[1], w.get_rng()[1])
     assert torch.equal(v.get_state(), w.get_state())

@@ -27,6 +27,7 @@ HostEnv *hs_create(const mhppo_env_cfg *cfg) {
   h->b.envd = (double *)calloc((size_t)E_ND * N, 8);
   h->b.envi = (int32_t *)calloc((size_t)EI_NI * N, 4);
   h->b.ev = (uint32_t *)calloc((size_t)EV_N * N, 4);
+  h->b.carb = (uint8_t *)calloc((size_t)2 * c.nC * N, 1);
   h->b.mt = (uint32_t *)calloc((size_t)MT_BLOCKS * MT_N * c.N + MT_PAD, 4);
   for (int e = 0; e < c.N; e++) env_seed_one(c, h->b, e);
   return h;
@@ -39,6 +40,7 @@ void hs_destroy(HostEnv *h) {
   free(h->b.envd);
   free(h->b.envi);
   free(h->b.ev);
+  free(h->b.carb);
   free(h->b.mt);
   delete h;
 }
