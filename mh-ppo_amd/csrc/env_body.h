@@ -15,9 +15,6 @@ constexpr int MAXS = 16;  // AV slots per env (scalable 2*nb_lines, coop nb_car)
 // shapes (stop 2/1/2, 4cars2 4/1/2).  Every other shape runs on the generic view.
 // (Multi-pedestrian shapes are left generic: fully unrolling ped_step per pedestrian
 // exceeds the unroller's budget and a runtime-indexed array would live in scratch.)
-#ifndef MHPPO_RESET_RNG_WIN
-#define MHPPO_RESET_RNG_WIN 16  // the reset / choix_test views' RNG window (Env's RK; A/B builds override)
-#endif
 #define MHPPO_REG_SHAPES(X) \
   X(V_COOP, 2, 2, 1) X(V_4CARS, 8, 4, 1) X(V_SCALABLE, 8, 8, 1) X(V_STOP, 2, 2, 1) X(V_4CARS2, 8, 4, 1)
 
@@ -179,7 +176,7 @@ MHPPO_HD void env_observe(EV &E, int mode, float *obs) {
 template <int V>
 MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
   // cross first: it sizes everything else (:844)
-  Env<V, MHPPO_RESET_RNG_WIN> E(c, b, e);
+  Env<V> E(c, b, e);
   E.hist_nf(0) = 0;  // every car's history = [0, 0] (car_init clears its own bits as well)
   E.hist_nf(1) = 0;
   E.cross = E.rng.uniform(c.xb0, c.xb1);
@@ -254,7 +251,7 @@ MHPPO_HD void env_reset_one(const Cfg &c, const Bufs &b, int e, float *obs) {
 // on that np.float32 speed; the reference's pinned NumPy 1.26 promotes to float64, as here.)
 template <int V>
 MHPPO_HD void env_choix_test_one(const Cfg &c, const Bufs &b, int e, float *obs) {
-  Env<V, MHPPO_RESET_RNG_WIN> E(c, b, e);
+  Env<V> E(c, b, e);
   const double v0 = (double)(float)(E.exists(0) != 0.0 ? E.car(C_VC, 0) : 0.0);
   E.cross = 3.0;
   E.cl = (double)c.nb_lines * E.cross;

@@ -427,10 +427,7 @@ struct PlainArr {
 // Env<V>: generic shapes.  Car/ped fields are read and written in place in HBM
 // (coalesced across the wave); used by reset, state dumps and every shape the
 // register view is not instantiated for.
-// RK: the RNG's register window (RngT<RK>; 0 = one global load per word).  The reset and
-// choix_test draws run with a window: their ~100 words per env then cost a few batched round trips
-// instead of one dependent load each (the same words in the same order).
-template <int V, int RK = 0>
+template <int V>
 struct Env {
   static constexpr int VAR = V;
   static constexpr int MAXAV = 16;
@@ -441,7 +438,7 @@ struct Env {
   const Cfg &c;
   const Bufs &b;
   int e;
-  RngT<RK> rng;
+  Rng rng;
   double cross, cl;  // crosswalk lane width, cross_lines = nb_lines * cross
 
   MHPPO_HD Env(const Cfg &c_, const Bufs &b_, int e_) : c(c_), b(b_), e(e_) {
