@@ -29,3 +29,10 @@ for k in range(K):
         print(f"  env {e}: fields {f[:12].tolist()} gpu {g[e][f[:4]].tolist()} oracle {o[e][f[:4]].tolist()} "
               f"mti gpu {int(mti_g[e])} oracle {int(mti_o[e])}")
 torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(20):
+    env.reset(want_obs=False)
+e1.record()
+torch.cuda.synchronize()
+print(f"reset time {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per reset ({N} envs)")
