@@ -852,13 +852,19 @@ __device__ __forceinline__ uint32_t pk_bf16(float x, float y) {  // one v_cvt_pk
   const f32x2 v = {x, y};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
+// x - (the bf16 in the low / high half of h, as f32): the residual of a split level (exact: x and
+// the bf16 rounding of x differ by a representable amount).  (One v_dot2c_f32_bf16 against
+// (-1, 0) / (0, -1) instead of the back-conversion + subtraction pair: 1 437 instead of 1 560
+// instructions per critic tile but +85 s_nop and +53 v_mov, train launch +6 %,
+// profiles/r06_x3/ab_dot2_split.txt, tools/patches/x3_r06_dot2_split.patch.)
+__device__ __forceinline__ float res_lo(uint32_t h, float x) { return x - __uint_as_float(h << 16); }
+__device__ __forceinline__ float res_hi(uint32_t h, float y) { return y - __uint_as_float(h & 0xffff0000u); }
 // (x, y) -> three packed bf16 pairs, x = hi + mid + lo exactly (element 0 in the low half)
 __device__ __forceinline__ void split_pair(float x, float y, uint32_t &h, uint32_t &m, uint32_t &lo) {
   h = pk_bf16(x, y);
-  const float x1 = x - __uint_as_float(h << 16), y1 = y - __uint_as_float(h & 0xffff0000u);
+  const float x1 = res_lo(h, x), y1 = res_hi(h, y);
   m = pk_bf16(x1, y1);
-  const float x2 = x1 - __uint_as_float(m << 16), y2 = y1 - __uint_as_float(m & 0xffff0000u);
-  lo = pk_bf16(x2, y2);
+  lo = pk_bf16(res_lo(m, x1), res_hi(m, y1));
 }
 // fragment element j = v[j]
 __device__ __forceinline__ F3 split8(const float *v) {
@@ -1198,14 +1204,14 @@ __device__ __forceinline__ void pin4(float *v) { asm volatile("" : "+v"(v[0]), "
 __device__ __forceinline__ void split_l1(const float *v, int q, F3 &f, float *r) {
   const uint32_t h = pk_bf16(v[2 * q], v[2 * q + 1]);
   f.p[0][q] = h;
-  r[2 * q] = v[2 * q] - __uint_as_float(h << 16);
-  r[2 * q + 1] = v[2 * q + 1] - __uint_as_float(h & 0xffff0000u);
+  r[2 * q] = res_lo(h, v[2 * q]);
+  r[2 * q + 1] = res_hi(h, v[2 * q + 1]);
 }
 // split levels 2-3 of pair q from its residuals (as split_pair: the same bits)
 __device__ __forceinline__ void split_l2(int q, F3 &f, const float *r) {
   const uint32_t m = pk_bf16(r[2 * q], r[2 * q + 1]);
   f.p[1][q] = m;
-  f.p[2][q] = pk_bf16(r[2 * q] - __uint_as_float(m << 16), r[2 * q + 1] - __uint_as_float(m & 0xffff0000u));
+  f.p[2][q] = pk_bf16(res_lo(m, r[2 * q]), res_hi(m, r[2 * q + 1]));
 }
 // ReLU-derivative mask of elements r, r + 1 of d by h > 0
 __device__ __forceinline__ void mask2(f32x16 &d, const f32x16 &h, int r) {
