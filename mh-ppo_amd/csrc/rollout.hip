@@ -44,7 +44,7 @@ __device__ inline void stage_weights(float *lds, const float *W, int n) {
 
 // -------------------------------------------------------------- begin
 // one lane per (env, slot, ped): choice features, choice actor, Categorical draw.
-// LDS: the actor's weights, then the observation rows of the block's envs (one flat coalesced copy:
+// LDS: the observation rows of the block's envs (one flat coalesced copy:
 // a lane's features read its env's row from LDS, not one strided global load per feature), then the
 // block's feature rows (row-per-lane, stride dc + 1: conflict-free), written to feat_d as ONE flat
 // coalesced run of TPB x dc floats after the forward (which reads its inputs from that LDS row).
@@ -53,22 +53,23 @@ __device__ inline void stage_weights(float *lds, const float *W, int n) {
 __host__ __device__ inline int choice_env_span(const Cfg &c) {  // envs a TPB-row block can touch
   return (TPB + c.nS * c.P - 1) / (c.nS * c.P) + 1;
 }
+// (The actor's weights are wave-uniform: read through the scalar cache as SGPR operands of the
+// fmaf chains — W is a separate __restrict__ argument, so the compiler may use scalar loads — not
+// staged in LDS, where every weight cost the LDS pipe a read per lane-group.)
 __host__ __device__ inline size_t choice_lds_floats(const Cfg &c, int n_in) {
-  return (size_t)mlp_size(n_in, 2) + (size_t)choice_env_span(c) * c.obs_dim + (size_t)TPB * (choice_dim(c) + 1);
+  return (size_t)choice_env_span(c) * c.obs_dim + (size_t)TPB * (choice_dim(c) + 1);
 }
 template <int V>
 __global__ void __launch_bounds__(TPB)
-    k_choice(Cfg c, mhppo_mlp m, const float *u, const int32_t *forced, mhppo_rollout_bufs B) {
+    k_choice(Cfg c, const float *__restrict__ W, const float *u, const int32_t *forced, mhppo_rollout_bufs B) {
   extern __shared__ float lds[];
   const ObsLayout L = obs_layout(c);
   const int dc = choice_dim(c), SP = c.nS * c.P, od = L.obs_dim;
   const size_t R = (size_t)c.N * SP, r0 = (size_t)blockIdx.x * TPB;
   const int nr = (int)min((size_t)TPB, R - r0);
-  const int nw = mlp_size(m.n_in, 2);
-  float *s_obs = lds + nw, *s_f = s_obs + (size_t)choice_env_span(c) * od;
+  float *s_obs = lds, *s_f = s_obs + (size_t)choice_env_span(c) * od;
   const size_t e0 = r0 / SP, e1 = (r0 + nr - 1) / SP;  // the block's envs [e0, e1]
   const int nobs = (int)(e1 - e0 + 1) * od;
-  for (int i = threadIdx.x; i < nw; i += TPB) lds[i] = m.packed[i];
   for (int i = threadIdx.x; i < nobs; i += TPB) s_obs[i] = B.obs[e0 * od + i];
   __syncthreads();
   const int t = threadIdx.x;
@@ -85,7 +86,10 @@ __global__ void __launch_bounds__(TPB)
       B.exist[e * c.nS + i] = L.scalable ? (uint8_t)(o[i * L.cw + 6] != 0.0f) : (uint8_t)1;
     }
     float pr[2];
-    mlp_forward<0, 2>(lds, dc, f, pr);
+    // the scalable 8-slot head (dc 54) and the coop / 4cars 4-slot one (27) fully unrolled
+    if (dc == 54) mlp_forward_rows<54, 2>(W, f, pr);
+    else if (dc == 27) mlp_forward_rows<27, 2>(W, f, pr);
+    else mlp_forward<0, 2>(W, dc, f, pr);
     // Softmax over the pair (Model_PPO type 2, :81-85)
     float mx = pr[0] > pr[1] ? pr[0] : pr[1];
     float ex0 = mhppo_expf(pr[0] - mx), ex1 = mhppo_expf(pr[1] - mx);
@@ -1315,7 +1319,7 @@ int mhppo_rollout_begin(mhppo_env *env, const mhppo_mlp *actor_choice, const flo
   size_t R = (size_t)c.N * c.nS * c.P;
   size_t shm = sizeof(float) * choice_lds_floats(c, actor_choice->n_in);
   if (shm > 160 * 1024) return set_error(MHPPO_EINVAL, "choice kernel LDS %zu B (obs_dim %d, dc %d)", shm, c.obs_dim, choice_dim(c));
-  VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, *actor_choice, u, forced_a, *bufs);
+  VLAUNCH(k_choice, c.variant, grid_for(R), shm, s, c, actor_choice->packed, u, forced_a, *bufs);
   size_t NS = (size_t)c.N * c.nS;
   if (bufs->rec_of) {  // the compact record layout: present segments ranked in (env, slot) order
     if (c.variant != V_SCALABLE) return set_error(MHPPO_EINVAL, "rec_of: the scalable env's layout only");

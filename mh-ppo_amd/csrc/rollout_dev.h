@@ -241,6 +241,47 @@ MHPPO_HD inline void mlp_forward(const float *W, int n_in, const float *x, float
   }
 }
 
+// mlp_forward's arithmetic (every output's fmaf chain in the same ascending order from 0, the bias
+// added last) for a compile-time input width, output-major and fully unrolled: with a wave-uniform
+// W each output's weight row is contiguous and streams through the scalar cache (the choice actor,
+// k_choice; hidden 2 kept whole before layer 3)
+template <int NIN, int NOUT>
+MHPPO_HD inline void mlp_forward_rows(const float *__restrict__ W, const float *x, float *out) {
+  const float *w1 = W, *b1 = w1 + 32 * NIN, *w2 = b1 + 32, *b2 = w2 + 64 * 32, *w3 = b2 + 64, *b3 = w3 + 32 * 64,
+              *w4 = b3 + 32, *b4 = w4 + NOUT * 32;
+  float xr[NIN], h1[32], h2[64], h3[32];
+#pragma unroll
+  for (int k = 0; k < NIN; k++) xr[k] = x[k];
+#pragma unroll
+  for (int o = 0; o < 32; o++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NIN; k++) acc = fmaf(w1[o * NIN + k], xr[k], acc);
+    h1[o] = relu(acc + b1[o]);
+  }
+#pragma unroll
+  for (int o2 = 0; o2 < 64; o2++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 32; k++) acc = fmaf(w2[o2 * 32 + k], h1[k], acc);
+    h2[o2] = relu(acc + b2[o2]);
+  }
+#pragma unroll
+  for (int o = 0; o < 32; o++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) acc = fmaf(w3[o * 64 + k], h2[k], acc);
+    h3[o] = relu(acc + b3[o]);
+  }
+#pragma unroll
+  for (int j = 0; j < NOUT; j++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 32; k++) acc = fmaf(w4[j * 32 + k], h3[k], acc);
+    out[j] = acc + b4[j];
+  }
+}
+
 // The same arithmetic (every output's fmaf chain in the same ascending order, bias
 // last) with the loops output-major, so each output reads its weights contiguously:
 // with a wave-uniform W they stream through the scalar cache as SGPR operands.
