@@ -242,14 +242,12 @@ MHPPO_HD inline void mlp_forward(const float *W, int n_in, const float *x, float
 }
 
 // mlp_forward's arithmetic (every output's fmaf chain in the same ascending order from 0, the bias
-// added last) for a compile-time input width, output-major and fully unrolled: with a wave-uniform
-// W each output's weight row is contiguous and streams through the scalar cache (the choice actor,
-// k_choice; hidden 2 kept whole before layer 3)
-#ifndef MHPPO_ROWS_UNROLL
-#define MHPPO_ROWS_UNROLL 32  // output loops of mlp_forward_rows unrolled this far (A/B builds override)
-#endif
-#define MHPPO_PRAGMA_(x) _Pragma(#x)
-#define MHPPO_UNROLL_N(n) MHPPO_PRAGMA_(unroll n)
+// added last) for a compile-time input width, output-major: with a wave-uniform W each output's
+// weight row is contiguous and streams through the scalar cache (the choice actor, k_choice; hidden
+// 2 kept whole before layer 3).  The per-output chains unrolled, the output loops not: fully
+// unrolled, the hoisted scalar loads spilled 516 SGPRs (k_choice at cfg4 247 us, unrolled by 4:
+// 252 us, rolled: 221 us; the LDS-staged generic forward before: 437 us,
+// profiles/r06_rollout/k_choice_variants.txt)
 template <int NIN, int NOUT>
 MHPPO_HD inline void mlp_forward_rows(const float *__restrict__ W, const float *x, float *out) {
   const float *w1 = W, *b1 = w1 + 32 * NIN, *w2 = b1 + 32, *b2 = w2 + 64 * 32, *w3 = b2 + 64, *b3 = w3 + 32 * 64,
@@ -257,21 +255,21 @@ MHPPO_HD inline void mlp_forward_rows(const float *__restrict__ W, const float *
   float xr[NIN], h1[32], h2[64], h3[32];
 #pragma unroll
   for (int k = 0; k < NIN; k++) xr[k] = x[k];
-  MHPPO_UNROLL_N(MHPPO_ROWS_UNROLL)
+#pragma unroll 1
   for (int o = 0; o < 32; o++) {
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < NIN; k++) acc = fmaf(w1[o * NIN + k], xr[k], acc);
     h1[o] = relu(acc + b1[o]);
   }
-  MHPPO_UNROLL_N(MHPPO_ROWS_UNROLL)
+#pragma unroll 1
   for (int o2 = 0; o2 < 64; o2++) {
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < 32; k++) acc = fmaf(w2[o2 * 32 + k], h1[k], acc);
     h2[o2] = relu(acc + b2[o2]);
   }
-  MHPPO_UNROLL_N(MHPPO_ROWS_UNROLL)
+#pragma unroll 1
   for (int o = 0; o < 32; o++) {
     float acc = 0.0f;
 #pragma unroll
