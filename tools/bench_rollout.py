@@ -28,4 +28,8 @@ with torch.no_grad():
         b.record()
         torch.cuda.synchronize()
         env_us = sum(e0.elapsed_time(e1) for e0, e1 in ev) / T * 1e3
-        print(f"iter {it}: collect {a.elapsed_time(b):.2f} ms, env kernel {env_us:.1f} us/step", flush=True)
+        g = algo.rollout.gpu
+        R = g.rows.numel() - 2 - 2 * (g.parts + 1)
+        nc, nw = (int(v) for v in g.rows[R:R + 2].tolist())
+        print(f"iter {it}: collect {a.elapsed_time(b):.2f} ms, env kernel {env_us:.1f} us/step; policy rows "
+              f"{nc} cross + {nw} wait of {R}", flush=True)
