@@ -232,13 +232,14 @@ __global__ void __launch_bounds__(TPB) k_policy_sorted(Cfg c, const float *__res
 // layer then feeds its inputs 2s, 2s + 1, i.e. every chain runs in ascending input order;
 // the 32 -> 1 output is the same ascending fmaf chain over both lane halves.
 #ifndef MHPPO_POLICY_BLOCKS_PER_CU
-#define MHPPO_POLICY_BLOCKS_PER_CU 2  // persistent k_policy_mfma blocks per CU (A/B builds override)
+#define MHPPO_POLICY_BLOCKS_PER_CU 4  // k_policy_mfma blocks resident per CU (A/B builds override)
 #endif
 #ifndef MHPPO_POLICY_TPB
-// k_policy_mfma block size: 8 waves share one LDS copy of the two actors, so two blocks per CU
-// give four waves per SIMD (<= 128 VGPRs) to hide the MFMA chains' layer-to-layer latency
-// (LDS per block: 38.7 KB of weights)
-#define MHPPO_POLICY_TPB 512
+// k_policy_mfma block size: 4 waves share one LDS copy of the two actors (38.7 KB), four blocks per CU
+// (the LDS bound) give four waves per SIMD (<= 128 VGPRs) to hide the MFMA chains' layer-to-layer
+// latency.  r06: 256-thread blocks, more of them than fit at once at large N (below), against
+// 512-thread blocks two per CU: cfg4 collect 10.85 -> 9.86 ms, cfg3 5.93 -> 5.80 ms
+#define MHPPO_POLICY_TPB 256
 #endif
 constexpr int PTPB = MHPPO_POLICY_TPB;
 namespace pol {
@@ -1377,7 +1378,7 @@ static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mh
   if (R > (size_t)INT32_MAX - 2) return set_error(MHPPO_EINVAL, "N*S*P too large");
   if (!bufs->rows) return set_error(MHPPO_EINVAL, "the policy step needs the head lists (bufs->rows)");
   if (!(bufs->flags & MHPPO_ROLLOUT_VALU_POLICY)) {
-    // persistent 32-row MFMA tiles: 2 blocks per CU
+    // persistent 32-row MFMA tiles (grid below)
     static int cus[mhppo::MAX_DEVICES] = {0};
     const int dev = env_device(env);
     if (dev < 0 || dev >= mhppo::MAX_DEVICES) return set_error(MHPPO_EINVAL, "device %d >= %d", dev, mhppo::MAX_DEVICES);
@@ -1388,7 +1389,12 @@ static int rollout_policy(mhppo_env *env, const mhppo_mlp *actor_cross, const mh
     }
     constexpr size_t WPB = PTPB / 64;  // waves per block
     const size_t tiles = R / (32 * (size_t)nparts) + 2;
-    const size_t blocks = std::min<size_t>((size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev] / nparts + 1,
+    // at least the blocks that fit at once (this part's share of them), at most one tile per wave, and
+    // beyond the resident blocks ~2 tiles per wave: the waiting blocks start as the first ones drain
+    // (cfg4's 8 192 tiles per part: 1 024 blocks, collect -9 %; cfg3: 513, -2 %; cfg2: 65 at one tile
+    // per wave, -7 %; profiles/r06_rollout/ab_policy_grid.txt)
+    const size_t resident = (size_t)MHPPO_POLICY_BLOCKS_PER_CU * cus[dev] / nparts + 1;
+    const size_t blocks = std::min<size_t>(std::max<size_t>(resident, (tiles + 2 * WPB - 1) / (2 * WPB)),
                                            (tiles + WPB - 1) / WPB);
     VLAUNCHB(k_policy_mfma, c.variant, dim3((unsigned)blocks), dim3(PTPB), 2 * pol::HEAD * sizeof(float),
              (hipStream_t)stream, c, actor_cross->packed, actor_wait->packed, actor_cross->mean, actor_cross->std,

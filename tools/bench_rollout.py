@@ -13,7 +13,7 @@ from mhppo.models import Model_PPO  # noqa: E402
 
 # ROLLOUT_CFG="variant nb_car nb_ped nb_lines" (default: the bench's config 3)
 _v, _nc, _np, _nl = (os.environ.get("ROLLOUT_CFG") or "4cars 4 1 2").split()
-venv = VecCrosswalk(_v, 65536, int(_nc), int(_np), int(_nl), seed_base=0)
+venv = VecCrosswalk(_v, int(os.environ.get("ROLLOUT_N", "65536")), int(_nc), int(_np), int(_nl), seed_base=0)
 torch.manual_seed(0)
 algo = Algo_PPO(Model_PPO, venv, verbose=False, seed=0)
 T = 80
