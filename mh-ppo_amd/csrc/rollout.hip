@@ -378,8 +378,16 @@ __device__ __forceinline__ float actor_tile(const float *Wl, const float (&f)[NF
 }
 }  // namespace pol
 
+// Registers for five waves per SIMD (88 VGPRs; 120 without the bound): the LDS holds four blocks per
+// CU, and the fifth slot lets a policy wave share a SIMD with a cfg4 env wave of the other rollout part
+// (k_sample_env_r<2, 8, 8, 1>: 404 VGPRs): collect cfg4 -0.9 %, cfg3 -0.6 %, cfg2 -1.4 %
+// (profiles/r06_rollout/ab_policy_vgpr.txt)
+#ifndef MHPPO_POLICY_WPE
+#define MHPPO_POLICY_WPE 5
+#endif
 template <int V>
-__global__ void __launch_bounds__(PTPB) k_policy_mfma(Cfg c, const float *__restrict__ Wc,
+__global__ void __launch_bounds__(PTPB) __attribute__((amdgpu_waves_per_eu(MHPPO_POLICY_WPE)))
+k_policy_mfma(Cfg c, const float *__restrict__ Wc,
                                                       const float *__restrict__ Ww, float mean_c, float std_c,
                                                       float mean_w, float std_w, mhppo_rollout_bufs B, Bufs eb,
                                                       int part, int nparts) {
