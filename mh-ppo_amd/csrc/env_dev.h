@@ -1184,53 +1184,81 @@ MHPPO_HD inline double car_reward(double Vc) { return -10. * pow_2(Vc - 10.0) / 
 template <int WAVES>
 __device__ __forceinline__ void mt_refill_wave(const Bufs &b, int N, int e, bool valid) {
   __shared__ uint32_t sh_a[WAVES][MT_N], sh_b[WAVES][MT_N];
+  constexpr int NQ = (MT_N + 63) / 64;  // words of one block per lane
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int mtb = valid ? b.envi[sidx(EI_NI, EI_MTB, e)] : 0;
   uint64_t stale = __ballot(valid && (mtb >> 2) != 0);
   if (!stale) return;
-  while (stale) {
-    const int l = __ffsll((unsigned long long)stale) - 1;
+  // The stale envs of the wave one after another, the next one's source block loaded (into
+  // registers) while the current one twists: its load latency overlaps the twist and the stores
+  // instead of opening every env's refill.
+  int ln = 0, el = 0, bl = 0, k = MT_BLOCKS;  // the current env's lane, id, ring state, first stale block
+  uint32_t nxt[NQ];
+  auto take = [&](int &l, int &el_, int &bl_, int &k_) {  // pop the next stale lane; load its source block
+    l = __ffsll((unsigned long long)stale) - 1;
     stale &= stale - 1;
-    const int el = __shfl(e, l), bl = __shfl(mtb, l);
-    uint32_t *blk = b.mt + (size_t)el * (MT_BLOCKS * MT_N);
-    const int a = mt_active(bl);
+    el_ = __shfl(e, l);
+    bl_ = __shfl(mtb, l);
+    const int a = mt_active(bl_);
+    k_ = 1;
+    while (k_ < MT_BLOCKS && !mt_stale(bl_, (a + k_) & 3)) k_++;  // first stale block in ring order
+    if (k_ == MT_BLOCKS) return;
+    const uint32_t *g_src = b.mt + (size_t)el_ * (MT_BLOCKS * MT_N) + ((a + k_ - 1) & 3) * MT_N;
+#pragma unroll
+    for (int i = 0; i < NQ; i++)
+      if (lane + 64 * i < MT_N) nxt[i] = g_src[lane + 64 * i];
+  };
+  take(ln, el, bl, k);
+  for (;;) {
     uint32_t *src = sh_a[w], *dst = sh_b[w];
-    int k = 1;
-    while (k < MT_BLOCKS && !mt_stale(bl, (a + k) & 3)) k++;  // first stale block in ring order
-    if (k == MT_BLOCKS) continue;
-    const uint32_t *g_src = blk + ((a + k - 1) & 3) * MT_N;
-    for (int q = lane; q < MT_N; q += 64) src[q] = g_src[q];
-    for (; k < MT_BLOCKS; k++) {
-    uint32_t *g_dst = blk + ((a + k) & 3) * MT_N;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = lane; q < 227; q += 64) dst[q] = src[q + 397] ^ mt_mix(src[q], src[q + 1]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = 227 + lane; q < 454; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = 454 + lane; q < 623; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) dst[623] = dst[396] ^ mt_mix(src[623], dst[0]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = lane; q < MT_N; q += 64) g_dst[q] = dst[q];
-    uint32_t *t = src;  // the new block is the next twist's source
-    src = dst;
-    dst = t;
+    if (k < MT_BLOCKS) {
+#pragma unroll
+      for (int i = 0; i < NQ; i++)
+        if (lane + 64 * i < MT_N) src[lane + 64 * i] = nxt[i];
     }
-    if (lane == l) b.envi[sidx(EI_NI, EI_MTB, el)] = a;  // active block kept, none stale
-    // the owning lane reads the new block later in this launch: stores complete first
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int l_c = ln, el_c = el, bl_c = bl, k_c = k;
+    const bool more = stale != 0;
+    if (more) take(ln, el, bl, k);  // the next env's block in flight during this one's twists
+    if (k_c < MT_BLOCKS) {
+      uint32_t *blk = b.mt + (size_t)el_c * (MT_BLOCKS * MT_N);
+      const int a = mt_active(bl_c);
+      for (int kk = k_c; kk < MT_BLOCKS; kk++) {
+        uint32_t *g_dst = blk + ((a + kk) & 3) * MT_N;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int q = lane; q < 227; q += 64) dst[q] = src[q + 397] ^ mt_mix(src[q], src[q + 1]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int q = 227 + lane; q < 454; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int q = 454 + lane; q < 623; q += 64) dst[q] = dst[q - 227] ^ mt_mix(src[q], src[q + 1]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) dst[623] = dst[396] ^ mt_mix(src[623], dst[0]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int q = lane; q < MT_N; q += 64) g_dst[q] = dst[q];
+        uint32_t *t = src;  // the new block is the next twist's source
+        src = dst;
+        dst = t;
+      }
+      if (lane == l_c) b.envi[sidx(EI_NI, EI_MTB, el_c)] = a;  // active block kept, none stale
+    }
+    // every lane has read this env's last LDS image before the next env's block overwrites sh_a
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!more) break;
   }
+  // the owning lanes read their new blocks later in this launch: stores complete first
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 #endif
 

@@ -20,7 +20,10 @@ T = 80
 with torch.no_grad():
     for it in range(3):
         ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(T)]
+        r0 = torch.cuda.Event(enable_timing=True); r1 = torch.cuda.Event(enable_timing=True)
+        r0.record()
         algo.rollout.reset()
+        r1.record()
         a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
         a.record()
         algo.rollout.gpu.collect(algo.actor_net_cross, algo.actor_net_wait, algo.actor_net_choice, seed=0,
@@ -31,5 +34,6 @@ with torch.no_grad():
         g = algo.rollout.gpu
         R = g.rows.numel() - 2 - 2 * (g.parts + 1)
         nc, nw = (int(v) for v in g.rows[R:R + 2].tolist())
-        print(f"iter {it}: collect {a.elapsed_time(b):.2f} ms, env kernel {env_us:.1f} us/step; policy rows "
+        print(f"iter {it}: reset {r0.elapsed_time(r1) * 1e3:.0f} us, collect {a.elapsed_time(b):.2f} ms, "
+              f"env kernel {env_us:.1f} us/step; policy rows "
               f"{nc} cross + {nw} wait of {R}", flush=True)
